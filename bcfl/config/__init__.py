@@ -1,0 +1,271 @@
+"""Dataclass configuration, reference-script presets and CLI parsing.
+
+The reference has no flag system: each script hard-codes ``DEVICE``, ``CHECKPOINT``,
+``NUM_CLIENTS`` and ``NUM_ROUNDS`` as module constants (``src/Servercase/server_IID_IMDB.py:47-50``,
+``src/Serverlesscase/serverless_cancer_biobert_allclients.py:37-41``) plus hard-coded
+hyper-parameters (lr 5e-5 at ``server_IID_IMDB.py:109``, batch 32 at ``:93``, 1 local epoch).
+Here every knob lives in :class:`FLConfig`; :data:`PRESETS` reproduces each reference script
+ and can be overridden from YAML or ``--key value`` CLI flags.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, List, Optional
+
+__all__ = ["FLConfig", "PRESETS", "get_preset", "parse_cli", "config_from_dict"]
+
+
+@dataclass
+class FLConfig:
+    # --- experiment shape -------------------------------------------------
+    mode: str = "serverless"            # "server" (FedAvg) | "serverless" (P2P gossip)
+    model: str = "bert-base"            # see bcfl.models.registry
+    dataset: str = "imdb"               # see bcfl.data.registry
+    num_labels: Optional[int] = None    # None -> dataset default
+    num_clients: int = 8
+    num_rounds: int = 20
+    local_epochs: int = 1
+    batch_size: int = 32
+    max_seq_len: int = 512
+    # --- data partitioning ---------------------------------------------------
+    partition: str = "label_shards"     # iid_random | ref_contiguous | label_shards | dirichlet | shared_random
+    train_samples: int = 240            # per client
+    test_samples: int = 60              # per client (local eval)
+    global_test_samples: int = 100      # global eval draw (reference load_data(): 100)
+    dirichlet_alpha: float = 0.5
+    resample_each_round: bool = False   # reference IID scripts draw a fresh random sample every round
+    # --- optimisation -----------------------------------------------------------
+    lr: float = 5e-5
+    weight_decay: float = 0.0
+    adam_betas: tuple = (0.9, 0.999)
+    adam_eps: float = 1e-6
+    adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
+    keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
+    dropout: Optional[float] = None     # None -> model default
+    dtype: str = "bf16"                 # compute dtype on GPU ("bf16" | "fp32")
+    # --- federation ------------------------------------------------------------
+    topology: str = "full"              # full | ring | pagerank (serverless neighbour graph)
+    mixing: str = "average"             # average (reference mean) | metropolis | choco
+    choco_gamma: float = 0.5
+    async_gossip: bool = True           # exchange on the side stream, mix stale-by-one replicas
+    wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
+    fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
+    server_wire_dtype: str = "fp32"
+    # --- trust layer -------------------------------------------------------------
+    anomaly_filter: str = "none"        # none | pagerank | modz | both
+    anomaly_k: float = 2.0              # reject below mean - k*std of PageRank
+    anomaly_modz_threshold: float = 3.5
+    sketch_dim: int = 8192
+    ledger: bool = True
+    topology_probe: bool = False        # measure xGMI bandwidth matrix and filter peers by PageRank
+    # --- fault injection -----------------------------------------------------------
+    inject_slow: Dict[int, float] = field(default_factory=dict)       # client -> ms
+    inject_byzantine: Dict[int, float] = field(default_factory=dict)  # client -> scale
+    # --- io / observability -----------------------------------------------------------
+    out_dir: str = "runs/default"
+    save_every: int = 1
+    save_clients: bool = False
+    compat_save_path: Optional[str] = None   # e.g. "my_albert_model2"
+    async_ckpt: bool = True
+    resume: Optional[str] = None
+    eval_local: bool = True
+    eval_global: bool = True
+    metrics_jsonl: bool = True
+    reference_prints: bool = True
+    profile: bool = False
+    deterministic: bool = False
+    seed: int = 42
+    device: str = "auto"                # auto | cuda | cpu
+    backend: str = "auto"               # auto | nccl | gloo
+    # --- reference-compat quirks ---------------------------------------
+    compat_chain: bool = False          # serverless clients train sequentially on ONE shared model
+    compat_bad_test_loss: bool = True   # loss = sum(batch means) / N (reference test())
+    unpad: bool = True                  # packed varlen batches (padding never computed)
+    vocab_size: Optional[int] = None
+    lora_rank: int = 16
+    lora_alpha: float = 32.0
+
+    def to_dict(self) -> Dict[str, Any]:
+        d = dataclasses.asdict(self)
+        d["adam_betas"] = list(self.adam_betas)
+        return d
+
+    def replace(self, **kw) -> "FLConfig":
+        return config_from_dict({**self.to_dict(), **kw})
+
+
+def config_from_dict(d: Dict[str, Any]) -> FLConfig:
+    names = {f.name for f in fields(FLConfig)}
+    unknown = set(d) - names
+    if unknown:
+        raise KeyError(f"unknown config keys: {sorted(unknown)}")
+    d = dict(d)
+    if "adam_betas" in d:
+        d["adam_betas"] = tuple(d["adam_betas"])
+    for k in ("inject_slow", "inject_byzantine"):
+        if k in d and d[k] is not None:
+            d[k] = {int(a): float(b) for a, b in dict(d[k]).items()}
+    return FLConfig(**d)
+
+
+# ---------------------------------------------------------------------------------------
+# Presets: one per reference script. ``compat`` presets reproduce
+# the reference sampling quirks; the four canonical names from the reference README
+# (README.md:2-5) are aliases of the IMDB scripts.
+# ---------------------------------------------------------------------------------------
+PRESETS: Dict[str, Dict[str, Any]] = {
+    # src/Servercase/server_IID_IMDB.py:47-50, :79-84, :188-190 — 20x20, shared random 100/100
+    "server_IID_IMDB": dict(mode="server", model="biobert", dataset="imdb", num_labels=2,
+                            num_clients=20, num_rounds=20, partition="shared_random",
+                            train_samples=100, test_samples=100, global_test_samples=100),
+    # src/Servercase/server_NonIID_IMDB.py:48, :83-84 — rows 0..240 of shuffled split, shared
+    "server_NonIID_IMDB": dict(mode="server", model="albert-base-v2", dataset="imdb", num_labels=2,
+                               num_clients=20, num_rounds=20, partition="label_shards",
+                               train_samples=240, test_samples=60),
+    # src/Servercase/server_iid_medical_transcirptions.py:28-31
+    "server_iid_medical_transcriptions": dict(mode="server", model="biobert", dataset="medical",
+                                              num_labels=40, num_clients=5, num_rounds=20,
+                                              partition="shared_random", train_samples=500,
+                                              test_samples=500),
+    # src/Servercase/server_noniid_medical_transcriptions.py:27-30, :219
+    "server_noniid_medical_transcriptions": dict(mode="server", model="biobert", dataset="medical",
+                                                 num_labels=40, num_clients=10, num_rounds=20,
+                                                 partition="ref_contiguous", train_samples=400,
+                                                 test_samples=400),
+    # src/Serverlesscase/serverless_IID_IMDB.py:29-33, :258 — fresh random 100/100 each round
+    "serverless_IID_IMDB": dict(mode="serverless", model="albert-base-v2", dataset="imdb",
+                                num_labels=2, num_clients=10, num_rounds=20, partition="iid_random",
+                                train_samples=100, test_samples=100, resample_each_round=True,
+                                compat_save_path="my_model.h5"),
+    # src/Serverlesscase/serverless_NonIID_IMDB.py:29-32, :59-60 — contiguous unshuffled shards
+    "serverless_NonIID_IMDB": dict(mode="serverless", model="albert-base-v2", dataset="imdb",
+                                   num_labels=2, num_clients=10, num_rounds=20,
+                                   partition="label_shards", train_samples=240, test_samples=60,
+                                   compat_save_path="my_albert_model2"),
+    # src/Serverlesscase/Serverless_NonIID_Medical_transcriptions.py:27-30, :55-56
+    "serverless_NonIID_medical_transcriptions": dict(mode="serverless", model="biobert",
+                                                     dataset="medical", num_labels=40,
+                                                     num_clients=10, num_rounds=20,
+                                                     partition="ref_contiguous",
+                                                     train_samples=400, test_samples=400,
+                                                     compat_save_path="medical_biobert"),
+    # src/Serverlesscase/Serverless_iid_Medical_transcriptions.py:27-30, :238
+    "serverless_iid_medical_transcriptions": dict(mode="serverless", model="biobert",
+                                                  dataset="medical", num_labels=40,
+                                                  num_clients=20, num_rounds=20,
+                                                  partition="iid_random", train_samples=500,
+                                                  test_samples=500, resample_each_round=True,
+                                                  compat_save_path="medical_biobert"),
+    # src/Serverlesscase/serverless_cancer_biobert_allclients.py:37-41 (sweep {5,10,20})
+    "serverless_cancer_biobert": dict(mode="serverless", model="biobert", dataset="cancer",
+                                      num_labels=41, num_clients=5, num_rounds=20,
+                                      partition="iid_random", train_samples=500, test_samples=500,
+                                      resample_each_round=True, compat_save_path="my_albert_model2"),
+    # src/Serverlesscase/serverless_caner_classification_iid.py:31-34
+    "serverless_cancer_albert_iid": dict(mode="serverless", model="albert-base-v2", dataset="cancer",
+                                         num_labels=41, num_clients=10, num_rounds=20,
+                                         partition="iid_random", train_samples=500,
+                                         test_samples=500, resample_each_round=True,
+                                         compat_save_path="my_albert_model2"),
+    # src/Serverlesscase/serverless_covid_iid.py:31-34
+    "serverless_covid_iid": dict(mode="serverless", model="albert-base-v2", dataset="covid",
+                                 num_labels=41, num_clients=10, num_rounds=20,
+                                 partition="iid_random", train_samples=500, test_samples=500,
+                                 resample_each_round=True, compat_save_path="my_albert_model2"),
+    # serverless_cancer_classification_with_BioBERT.ipynb:749-753 — the only measured run (A100)
+    "serverless_cancer_biobert_notebook": dict(mode="serverless", model="biobert", dataset="cancer",
+                                               num_labels=41, num_clients=2, num_rounds=2,
+                                               partition="iid_random", train_samples=500,
+                                               test_samples=500, resample_each_round=True),
+    # BASELINE.json configs --------------------------------------------------------------
+    "baseline1_distilbert_server_iid_cpu": dict(mode="server", model="distilbert", dataset="imdb",
+                                                num_labels=2, num_clients=2, num_rounds=2,
+                                                partition="iid_random", train_samples=100,
+                                                test_samples=100, device="cpu", backend="gloo",
+                                                dtype="fp32"),
+    "baseline2_bert_server_iid": dict(mode="server", model="bert-base", dataset="imdb", num_labels=2,
+                                      num_clients=8, num_rounds=20, partition="iid_random",
+                                      train_samples=100, test_samples=100),
+    "baseline3_bert_serverless_noniid": dict(mode="serverless", model="bert-base", dataset="imdb",
+                                             num_labels=2, num_clients=8, num_rounds=20,
+                                             partition="label_shards", train_samples=240,
+                                             test_samples=60, async_gossip=True),
+    "baseline4_biobert_serverless_noniid_trust": dict(mode="serverless", model="biobert",
+                                                      dataset="imdb", num_labels=2, num_clients=8,
+                                                      num_rounds=20, partition="label_shards",
+                                                      train_samples=240, test_samples=60,
+                                                      anomaly_filter="both", ledger=True,
+                                                      topology="pagerank"),
+    "baseline5_llama3_8b_lora_serverless": dict(mode="serverless", model="llama3-8b-lora",
+                                                dataset="imdb", num_labels=2, num_clients=8,
+                                                num_rounds=20, partition="label_shards",
+                                                train_samples=240, test_samples=60, batch_size=8,
+                                                max_seq_len=512, lr=2e-4),
+}
+
+# README.md:2-5 canonical entry-point names
+PRESETS["server_IID"] = PRESETS["server_IID_IMDB"]
+PRESETS["server_NonIID"] = PRESETS["server_NonIID_IMDB"]
+PRESETS["serverless_IID"] = PRESETS["serverless_IID_IMDB"]
+PRESETS["serverless_NonIID"] = PRESETS["serverless_NonIID_IMDB"]
+
+
+def get_preset(name: str, **overrides) -> FLConfig:
+    if name not in PRESETS:
+        raise KeyError(f"unknown preset {name!r}; known: {sorted(PRESETS)}")
+    return config_from_dict({**PRESETS[name], **overrides})
+
+
+def _coerce(field_type: Any, default: Any, raw: str) -> Any:
+    if raw.lower() in ("none", "null"):
+        return None
+    if isinstance(default, bool) or field_type in (bool, "bool"):
+        return raw.lower() in ("1", "true", "yes", "on")
+    if isinstance(default, int) and not isinstance(default, bool):
+        return int(raw)
+    if isinstance(default, float):
+        return float(raw)
+    if isinstance(default, (dict, list, tuple)):
+        if isinstance(default, dict) and ":" in raw and not raw.strip().startswith("{"):
+            out = {}
+            for item in raw.split(","):
+                a, b = item.split(":")
+                out[int(a)] = float(b)
+            return out
+        return json.loads(raw)
+    if field_type in ("Optional[int]",) or "int" in str(field_type) and "Optional" in str(field_type):
+        return int(raw)
+    return raw
+
+
+def parse_cli(argv: Optional[List[str]] = None, default_preset: Optional[str] = None) -> FLConfig:
+    """``--preset NAME --config file.yaml --key value ...`` -> FLConfig."""
+    p = argparse.ArgumentParser(description="bcfl federated fine-tuning")
+    p.add_argument("--preset", default=default_preset)
+    p.add_argument("--config", default=None, help="YAML file with FLConfig keys")
+    for f in fields(FLConfig):
+        p.add_argument("--" + f.name.replace("_", "-"), dest=f.name, default=None)
+    args = p.parse_args(argv)
+    base: Dict[str, Any] = {}
+    if args.preset:
+        base.update(PRESETS[args.preset])
+    if args.config:
+        import yaml
+        with open(args.config) as fh:
+            base.update(yaml.safe_load(fh) or {})
+    defaults = FLConfig()
+    for f in fields(FLConfig):
+        raw = getattr(args, f.name)
+        if raw is None:
+            continue
+        default = base.get(f.name, getattr(defaults, f.name))
+        if default is None and f.name in ("num_labels", "vocab_size"):
+            base[f.name] = int(raw)
+        elif default is None and f.name == "dropout":
+            base[f.name] = float(raw)
+        else:
+            base[f.name] = _coerce(f.type, default, raw)
+    return config_from_dict(base)

@@ -1,0 +1,155 @@
+"""Packed (varlen) batches and the per-client loader.
+
+The reference pads every batch to its longest row with ``DataCollatorWithPadding``
+(``src/Servercase/server_IID_IMDB.py:89-99``) and moves each batch host->device inside the hot
+loop (``serverless_IID_IMDB.py:162``). Here a batch is *packed*: the valid tokens of all rows
+back to back plus ``cu_seqlens`` (row boundaries), so no kernel ever computes a pad position.
+All int32 fields of an epoch are laid out in ONE pinned host buffer and moved with ONE
+asynchronous H2D copy; batches are views into the device copy.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterator, List, Optional
+
+import numpy as np
+import torch
+
+from .synthetic import TokenDataset
+
+__all__ = ["PackedBatch", "PaddedBatch", "make_packed_batch", "make_padded_batch", "ClientLoader"]
+
+
+@dataclass
+class PackedBatch:
+    input_ids: torch.Tensor     # [T] int32
+    position_ids: torch.Tensor  # [T] int32
+    cu_seqlens: torch.Tensor    # [B+1] int32
+    labels: torch.Tensor        # [B] int32
+    max_seqlen: int
+    seq_lens: np.ndarray        # host copy of row lengths
+    cu_host: np.ndarray         # host copy of cu_seqlens
+
+    @property
+    def batch_size(self) -> int:
+        return int(self.seq_lens.shape[0])
+
+    @property
+    def num_tokens(self) -> int:
+        return int(self.cu_host[-1])
+
+    def to(self, device, non_blocking: bool = True) -> "PackedBatch":
+        return PackedBatch(self.input_ids.to(device, non_blocking=non_blocking),
+                           self.position_ids.to(device, non_blocking=non_blocking),
+                           self.cu_seqlens.to(device, non_blocking=non_blocking),
+                           self.labels.to(device, non_blocking=non_blocking),
+                           self.max_seqlen, self.seq_lens, self.cu_host)
+
+
+@dataclass
+class PaddedBatch:
+    input_ids: torch.Tensor       # [B, S] int64
+    attention_mask: torch.Tensor  # [B, S] int64
+    labels: torch.Tensor          # [B]
+
+
+def _gather(ds: TokenDataset, idx: np.ndarray):
+    lens = ds.lengths[idx]
+    cu = np.zeros(len(idx) + 1, dtype=np.int64)
+    np.cumsum(lens, out=cu[1:])
+    starts = ds.offsets[idx]
+    # flat gather index: start_of_row + position_in_row
+    pos = np.arange(cu[-1], dtype=np.int64) - np.repeat(cu[:-1], lens)
+    flat = np.repeat(starts, lens) + pos
+    return ds.tokens[flat], pos, cu, lens
+
+
+def make_packed_batch(ds: TokenDataset, idx: np.ndarray) -> PackedBatch:
+    toks, pos, cu, lens = _gather(ds, np.asarray(idx, dtype=np.int64))
+    return PackedBatch(torch.from_numpy(toks.astype(np.int32)),
+                       torch.from_numpy(pos.astype(np.int32)),
+                       torch.from_numpy(cu.astype(np.int32)),
+                       torch.from_numpy(ds.labels[idx].astype(np.int32)),
+                       int(lens.max()) if len(lens) else 0, lens, cu)
+
+
+def make_padded_batch(ds: TokenDataset, idx: np.ndarray, pad_id: int = 0) -> PaddedBatch:
+    idx = np.asarray(idx, dtype=np.int64)
+    lens = ds.lengths[idx]
+    S = int(lens.max())
+    ids = np.full((len(idx), S), pad_id, dtype=np.int64)
+    mask = np.zeros((len(idx), S), dtype=np.int64)
+    for r, i in enumerate(idx):
+        row = ds.row(int(i))
+        ids[r, : len(row)] = row
+        mask[r, : len(row)] = 1
+    return PaddedBatch(torch.from_numpy(ids), torch.from_numpy(mask),
+                       torch.from_numpy(ds.labels[idx].astype(np.int64)))
+
+
+class ClientLoader:
+    """Epoch iterator over one client's rows (train: shuffled like ``DataLoader(shuffle=True)``)."""
+
+    def __init__(self, ds: TokenDataset, indices: np.ndarray, batch_size: int = 32,
+                 shuffle: bool = False, seed: int = 0):
+        self.ds = ds
+        self.indices = np.asarray(indices, dtype=np.int64)
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.seed = seed
+        self.epoch = 0
+
+    def __len__(self) -> int:  # number of batches (Flower's num_examples quirk uses this)
+        return (len(self.indices) + self.batch_size - 1) // self.batch_size
+
+    @property
+    def num_examples(self) -> int:
+        return int(len(self.indices))
+
+    def _order(self, epoch: Optional[int] = None) -> np.ndarray:
+        e = self.epoch if epoch is None else epoch
+        if not self.shuffle:
+            return self.indices
+        r = np.random.default_rng([self.seed, e])
+        return self.indices[r.permutation(len(self.indices))]
+
+    def host_batches(self, epoch: Optional[int] = None) -> List[PackedBatch]:
+        order = self._order(epoch)
+        return [make_packed_batch(self.ds, order[i:i + self.batch_size])
+                for i in range(0, len(order), self.batch_size)]
+
+    def device_batches(self, device, epoch: Optional[int] = None) -> List[PackedBatch]:
+        """All batches of one epoch, staged with ONE pinned-buffer H2D copy."""
+        hb = self.host_batches(epoch)
+        self.epoch += 1
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            return hb
+        sizes = []
+        for b in hb:
+            sizes += [b.input_ids.numel(), b.position_ids.numel(), b.cu_seqlens.numel(),
+                      b.labels.numel()]
+        total = int(sum(sizes))
+        host = torch.empty(total, dtype=torch.int32, pin_memory=True)
+        off = 0
+        for b in hb:
+            for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
+                n = t.numel()
+                host[off:off + n].copy_(t.reshape(-1))
+                off += n
+        devbuf = host.to(dev, non_blocking=True)
+        out, off = [], 0
+        for b in hb:
+            views = []
+            for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
+                n = t.numel()
+                views.append(devbuf[off:off + n])
+                off += n
+            out.append(PackedBatch(views[0], views[1], views[2], views[3], b.max_seqlen,
+                                   b.seq_lens, b.cu_host))
+        self._keepalive = (host, devbuf)
+        return out
+
+    def __iter__(self) -> Iterator[PackedBatch]:
+        yield from self.host_batches()
+        self.epoch += 1

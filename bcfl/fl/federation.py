@@ -1,0 +1,534 @@
+"""The federation runner: server FedAvg and serverless (async) P2P gossip on one client per GPU.
+
+Reference call stacks:
+
+* server (§3.1): Flower ``start_simulation`` with ``FedAvg(fraction_fit=1, fraction_evaluate=1,
+  evaluate_metrics_aggregation_fn=weighted_average)`` (``src/Servercase/server_IID_IMDB.py:199-218``)
+  -> here :meth:`Federation.server_round`: every rank trains its client(s) from the global model,
+  the weighted sum Σ n_k w_k / Σ n is ONE RCCL all-reduce of the fp32 flat buffer, client-side
+  evaluation of the new global model is aggregated with ``weighted_average``.
+* serverless (§3.2): the sequential chain + host mean of ``serverless_*.py:284-318``
+  -> :meth:`Federation.serverless_round`: clients train concurrently (one per GPU), exchange over
+  RCCL send/recv (:class:`bcfl.parallel.gossip.GossipEngine`), async by default, and mix.
+  ``compat_chain=True`` reproduces the reference chain exactly (single process).
+
+Around both: partitioning (IID / reference contiguous / label shards / Dirichlet), update anomaly
+filtering, the hash-chained ledger, async HF-layout checkpoints, metrics JSONL and the reference's
+console lines.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+import zlib
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ckpt import AsyncCheckpointer, dir_size_gb, mirror_dir, load_into
+from ..config import FLConfig
+from ..data.batching import ClientLoader
+from ..data.partition import global_test_indices, partition_clients
+from ..data.registry import get_dataset, load_split
+from ..models import build_model, model_config, special_tokens
+from ..parallel import dist as D
+from ..parallel.flat import FlatAdamW, FlatParams
+from ..parallel.gossip import GossipEngine
+from ..parallel.topology import clients_of_rank, mixing_matrix, neighbours
+from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
+from ..trust.ledger import Ledger
+from ..utils.obs import MetricsWriter, PhaseTimer, Telemetry
+from .trainer import EvalResult, LocalTrainer
+
+DATA_SEED = 1234
+
+
+def _cseed(seed: int, c: int) -> int:
+    return zlib.crc32(f"{seed}:{c}".encode()) & 0x7FFFFFFF
+
+
+def weighted_average(metrics):
+    """Reference metric aggregation (``server_IID_IMDB.py:199-203``): Σ n_k·m_k / Σ n_k."""
+    ex = sum(n for n, _ in metrics)
+    out = {}
+    for key in ("accuracy", "loss"):
+        vals = [n * m[key] for n, m in metrics if key in m]
+        if vals:
+            out[key] = sum(vals) / max(ex, 1)
+    return out
+
+
+class Federation:
+    def __init__(self, cfg: FLConfig, verbose: bool = True):
+        self.cfg = cfg
+        self.rt = D.init_runtime(cfg.device, cfg.backend)
+        self.device = self.rt.device
+        self.is_cuda = self.device.type == "cuda"
+        self.verbose = verbose and self.rt.is_main
+        self.dtype = torch.bfloat16 if (self.is_cuda and cfg.dtype == "bf16") else torch.float32
+        self.telemetry = Telemetry()
+        # ---------------- data --------------------------------------------------------------
+        self.spec = get_dataset(cfg.dataset)
+        cls_id, sep_id, vocab = special_tokens(cfg.model)
+        vocab = cfg.vocab_size or vocab
+        _, mcfg = model_config(cfg.model)
+        self.max_len = min(cfg.max_seq_len, getattr(mcfg, "max_position_embeddings", cfg.max_seq_len))
+        self.train_ds = load_split(cfg.dataset, "train", vocab, self.max_len, DATA_SEED, cls_id, sep_id)
+        self.test_ds = load_split(cfg.dataset, "test", vocab, self.max_len, DATA_SEED, cls_id, sep_id)
+        self.num_labels = cfg.num_labels or self.spec.num_classes
+        self._parts: Dict[int, list] = {}
+        # ---------------- model + flat buffers ------------------------------------------------
+        mdtype = self.dtype if not cfg.model.startswith("llama") else (
+            torch.bfloat16 if self.is_cuda else torch.float32)
+        self.model = build_model(cfg.model, self.num_labels, device=self.device, dtype=mdtype,
+                                 dropout=cfg.dropout, vocab_size=vocab, seed=cfg.seed,
+                                 lora_rank=cfg.lora_rank, lora_alpha=cfg.lora_alpha)
+        self.flat = FlatParams.from_model(self.model, self.device, mdtype)
+        if self.rt.distributed:
+            D.broadcast_(self.flat.master, 0)
+            self.flat.sync_param_from_master()
+        self.opt = FlatAdamW(self.flat, cfg.lr, cfg.adam_betas, cfg.adam_eps, cfg.weight_decay,
+                             cfg.adam_mode)
+        self.trainer = LocalTrainer(self.model, self.flat, self.opt)
+        # ---------------- clients ---------------------------------------------------------------
+        n = cfg.num_clients
+        self.local_clients = clients_of_rank(self.rt.rank, self.rt.world, n)
+        self.multi = len(self.local_clients) > 1
+        if cfg.compat_chain and self.rt.world > 1:
+            raise ValueError("compat_chain reproduces the reference's single-process chain; world must be 1")
+        self.client_rng = {c: {"seed": _cseed(cfg.seed, c), "counter": 0} for c in self.local_clients}
+        self.client_opt: Dict[int, dict] = {}
+        self.client_master: Dict[int, torch.Tensor] = {}
+        if cfg.mode == "serverless" and self.multi and not cfg.compat_chain:
+            for c in self.local_clients:
+                self.client_master[c] = self.flat.master.detach().clone()
+        self.global_master: Optional[torch.Tensor] = None
+        if cfg.mode == "server":
+            self.global_master = self.flat.master.detach().clone()
+            self.acc = torch.zeros_like(self.flat.master)
+        # ---------------- gossip -------------------------------------------------------------------
+        self.excluded: List[int] = []
+        self.gossip: Optional[GossipEngine] = None
+        if cfg.mode == "serverless" and not cfg.compat_chain:
+            if cfg.topology_probe and self.rt.distributed:
+                from ..trust.probe import probe_and_filter
+                self.excluded = probe_and_filter(self.flat.param, n)
+            self.nbrs = neighbours(cfg.topology, n, self.excluded)
+            states = ({c: self.client_master[c] for c in self.local_clients} if self.multi
+                      else {self.local_clients[0]: self.flat.master})
+            wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
+            if cfg.wire_dtype == "bf16_raw":
+                wire = "bf16"
+            self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip)
+            self.gossip.seed_replicas(self.flat.master)
+        # ---------------- trust ---------------------------------------------------------------------
+        self.filter = UpdateAnomalyFilter(cfg.anomaly_filter, cfg.anomaly_k,
+                                          cfg.anomaly_modz_threshold) if cfg.anomaly_filter != "none" else None
+        self.prev_verdicts = Verdicts()
+        out = cfg.out_dir
+        self.ledger = Ledger(genesis={"model": cfg.model, "mode": cfg.mode, "clients": n,
+                                      "dataset": cfg.dataset, "partition": cfg.partition},
+                             path=os.path.join(out, "ledger.jsonl") if (cfg.ledger and self.rt.is_main) else None,
+                             ts=0.0) if cfg.ledger else None
+        # ---------------- io ---------------------------------------------------------------------------
+        self.metrics = MetricsWriter(os.path.join(out, "metrics.jsonl"),
+                                     cfg.metrics_jsonl and self.rt.is_main, append=bool(cfg.resume))
+        self.ckpt = AsyncCheckpointer(self.model, self.flat, cfg.async_ckpt) if (
+            cfg.save_every > 0 and (self.rt.is_main or cfg.save_clients)) else None
+        self.timer = PhaseTimer(sync_device=cfg.profile)
+        self.global_accuracies: List[float] = []
+        self.history: List[dict] = []
+        self.start_round = 0
+        self.tokens_trained = 0
+        if cfg.resume:
+            self._resume(cfg.resume)
+
+    # ================================ helpers ==================================================
+    def log(self, *a):
+        if self.verbose:
+            print(*a, flush=True)
+
+    def partitions(self, r: int):
+        key = r if self.cfg.resample_each_round else 0
+        if key not in self._parts:
+            c = self.cfg
+            self._parts = {key: partition_clients(c.partition, self.spec, self.train_ds.labels,
+                                                  self.test_ds.labels, c.num_clients,
+                                                  c.train_samples, c.test_samples, c.seed, key,
+                                                  c.dirichlet_alpha)}
+        return self._parts[key]
+
+    def client_examples(self, c: int, r: int) -> int:
+        return int(len(self.partitions(r)[c].train))
+
+    def fedavg_weight_counts(self, r: int) -> np.ndarray:
+        n = self.cfg.num_clients
+        if self.cfg.fedavg_weighting == "uniform":
+            return np.ones(n)
+        ex = np.array([self.client_examples(c, r) for c in range(n)], dtype=np.float64)
+        if self.cfg.fedavg_weighting == "batches":  # Flower quirk: len(trainloader) (C10)
+            return np.ceil(ex / self.cfg.batch_size)
+        return ex
+
+    def train_batches(self, c: int, r: int, epoch: int):
+        sp = self.partitions(r)[c]
+        ld = ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
+                          seed=_cseed(self.cfg.seed, c))
+        return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
+
+    def test_batches(self, c: int, r: int):
+        sp = self.partitions(r)[c]
+        return ClientLoader(self.test_ds, sp.test, self.cfg.batch_size).device_batches(self.device)
+
+    def global_test_batches(self, r: int):
+        idx = global_test_indices(len(self.test_ds), self.cfg.global_test_samples, self.cfg.seed,
+                                  r if self.cfg.resample_each_round else None)
+        mine = idx[self.rt.rank::self.rt.world]
+        if len(mine) == 0:
+            return []
+        return ClientLoader(self.test_ds, mine, self.cfg.batch_size).device_batches(self.device)
+
+    def _activate(self, c: int, master: Optional[torch.Tensor] = None):
+        if master is not None:
+            self.flat.load_master(master)
+        elif self.multi and c in self.client_master:
+            self.flat.load_master(self.client_master[c])
+        if self.cfg.keep_optimizer_state and c in self.client_opt:
+            self.opt.load_state_dict(self.client_opt[c])
+        else:
+            self.opt.reset()
+        ops.rng.global_rng().load_state(self.client_rng[c])
+
+    def _deactivate(self, c: int):
+        if self.multi and c in self.client_master:
+            self.client_master[c].copy_(self.flat.master)
+        if self.cfg.keep_optimizer_state:
+            self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
+                                  for k, v in self.opt.state_dict().items()}
+        self.client_rng[c] = ops.rng.global_rng().state()
+
+    def _train_client(self, c: int, r: int) -> Dict[str, float]:
+        out = {"loss_sum": 0.0, "batches": 0, "tokens": 0, "examples": 0}
+        loss_t = None
+        for e in range(self.cfg.local_epochs):
+            with self.timer.phase("data"):
+                batches = self.train_batches(c, r, e)
+            with self.timer.phase("train"):
+                res = self.trainer.train_epoch(batches)
+            loss_t = res["loss_sum"] if loss_t is None else loss_t + res["loss_sum"]
+            for k in ("batches", "tokens", "examples"):
+                out[k] += res[k]
+        out["loss_t"] = loss_t
+        self.tokens_trained += out["tokens"]
+        if c in self.cfg.inject_slow:
+            time.sleep(self.cfg.inject_slow[c] / 1000.0)
+        return out
+
+    @torch.no_grad()
+    def _inject_byzantine(self, c: int, ref: torch.Tensor):
+        s = self.cfg.inject_byzantine.get(c)
+        if s is None:
+            return
+        m = self.flat.master
+        m.sub_(ref).mul_(s).add_(ref)
+        self.flat.sync_param_from_master()
+
+    @torch.no_grad()
+    def _update_stats(self, ref: torch.Tensor):
+        d = self.flat.master - ref
+        return ops.block_sketch(d, self.cfg.sketch_dim).float(), d.norm().float()
+
+    def _verdicts(self, sk_local: Dict[int, torch.Tensor], nrm_local: Dict[int, torch.Tensor]) -> Verdicts:
+        if self.filter is None:
+            return Verdicts()
+        n = self.cfg.num_clients
+        dim = self.cfg.sketch_dim
+        mine = torch.zeros(n, dim + 1, dtype=torch.float32, device=self.device)
+        for c in sk_local:
+            mine[c, :dim] = sk_local[c]
+            mine[c, dim] = nrm_local[c]
+        D.all_reduce_(mine)  # each client row is written by exactly one rank
+        a = mine.cpu().numpy()
+        return self.filter(a[:, :dim], a[:, dim])
+
+    def _merkle(self) -> str:
+        return ops.merkle_root_sha256(self.flat.master).hex()
+
+    def _ledger_round(self, r: int, recs: List[dict], extra: Optional[dict] = None):
+        if self.ledger is None:
+            return
+        with self.timer.phase("ledger"):
+            allrecs = [x for part in D.all_gather_object(recs) for x in part]
+            allrecs.sort(key=lambda x: x["client"])
+            for x in allrecs:
+                self.ledger.append(r, x["client"], "update", x["root"], x["verdict"],
+                                   x.get("metrics", {}), ts=x["ts"])
+            if extra is not None:
+                self.ledger.append(r, -1, extra.pop("kind", "round"), extra.pop("root", ""),
+                                   "accept", extra, ts=float(r + 1))
+            self.ledger.flush()
+
+    def _eval_global(self, r: int) -> EvalResult:
+        with self.timer.phase("eval_global"):
+            gb = self.global_test_batches(r)
+            acc = self.trainer.evaluate_device(gb) if gb else torch.zeros(4, dtype=torch.float64, device=self.device)
+            D.all_reduce_(acc)
+            a = acc.cpu().tolist()
+        return EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+
+    # ================================ rounds ====================================================
+    def server_round(self, r: int) -> dict:
+        cfg = self.cfg
+        G = self.global_master
+        counts = self.fedavg_weight_counts(r)
+        recs, sk, nr, trained, losses = [], {}, {}, {}, {}
+        need_copy = self.filter is not None and self.multi
+        self.acc.zero_()
+        w_all = counts / counts.sum()
+        for c in self.local_clients:
+            self._activate(c, master=G)
+            if self.verbose and cfg.reference_prints:
+                print("Training Started...", flush=True)
+            st = self._train_client(c, r)
+            self._inject_byzantine(c, G)
+            if self.verbose and cfg.reference_prints:
+                print("Training Finished.", flush=True)
+            losses[c] = st
+            if self.filter is not None:
+                with self.timer.phase("anomaly"):
+                    sk[c], nr[c] = self._update_stats(G)
+            root = self._merkle() if self.ledger is not None else ""
+            recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
+                         "verdict": "accept", "metrics": {"examples": st["examples"]}})
+            if need_copy:
+                trained[c] = self.flat.master.detach().clone()
+            elif self.filter is None:
+                ops.weighted_accumulate_(self.acc, self.flat.master, float(w_all[c]))
+            else:
+                trained[c] = self.flat.master
+            self._deactivate(c)
+        with self.timer.phase("anomaly"):
+            v = self._verdicts(sk, nr)
+        if self.filter is not None:
+            mask = np.array([0.0 if c in v.rejected else 1.0 for c in range(cfg.num_clients)])
+            w = counts * mask
+            w = w / max(w.sum(), 1e-30)
+            for c in self.local_clients:
+                ops.weighted_accumulate_(self.acc, trained[c], float(w[c]))
+            for x in recs:
+                x["verdict"] = v.verdict(x["client"])
+        with self.timer.phase("comm"):
+            D.all_reduce_(self.acc)
+        G.copy_(self.acc)
+        self.flat.load_master(G)
+        # Flower evaluate_round: every client evaluates the new global model on its test split
+        client_metrics = []
+        if cfg.eval_local:
+            with self.timer.phase("eval_local"):
+                dev_res = {}
+                for c in self.local_clients:
+                    dev_res[c] = self.trainer.evaluate_device(self.test_batches(c, r))
+                loc = []
+                for c, t in dev_res.items():
+                    a = t.cpu().tolist()
+                    e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+                    loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
+                client_metrics = [x for part in D.all_gather_object(loc) for x in part]
+        agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
+        ge = self._eval_global(r) if cfg.eval_global else None
+        train_loss = self._reduce_train_loss(losses)
+        self._ledger_round(r, recs, {"kind": "global", "root": self._merkle() if self.ledger else "",
+                                     "rejected": sorted(v.rejected)})
+        return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
+                "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
+                "client_metrics": client_metrics, "bytes_sent": float(self.flat.nbytes("master"))}
+
+    def _reduce_train_loss(self, losses: Dict[int, dict]) -> float:
+        if not losses:
+            return 0.0
+        t = torch.zeros(2, dtype=torch.float64, device=self.device)
+        for st in losses.values():
+            if st["loss_t"] is not None:
+                t[0] += st["loss_t"].double()
+            t[1] += st["batches"]
+        D.all_reduce_(t)
+        a = t.cpu().tolist()
+        return a[0] / max(a[1], 1)
+
+    def serverless_round(self, r: int) -> dict:
+        cfg = self.cfg
+        if cfg.compat_chain:
+            return self._chain_round(r)
+        recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
+        need_prev = self.filter is not None or bool(cfg.inject_byzantine)
+        for c in self.local_clients:
+            self._activate(c)
+            prev = self.flat.master.detach().clone() if need_prev else None
+            st = self._train_client(c, r)
+            if prev is not None:
+                self._inject_byzantine(c, prev)
+                if self.filter is not None:
+                    with self.timer.phase("anomaly"):
+                        sk[c], nr[c] = self._update_stats(prev)
+            losses[c] = st
+            if cfg.eval_local:
+                with self.timer.phase("eval_local"):
+                    local_eval[c] = self.trainer.evaluate_device(self.test_batches(c, r))
+            root = self._merkle() if self.ledger is not None else ""
+            recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
+                         "verdict": "accept", "metrics": {"examples": st["examples"]}})
+            self._deactivate(c)
+        with self.timer.phase("anomaly"):
+            v = self._verdicts(sk, nr)
+        for x in recs:
+            x["verdict"] = v.verdict(x["client"])
+        # async mixes states published last round -> apply last round's verdicts to them
+        use_v = self.prev_verdicts if cfg.async_gossip else v
+        W = mixing_matrix(self.nbrs, cfg.mixing, use_v.rejected)
+        with self.timer.phase("comm"):
+            info = self.gossip.end_of_round(r, W, None if self.multi else {self.local_clients[0]: self.flat.param})
+        self.prev_verdicts = v
+        if self.multi:  # evaluate this rank's first client's mixed model
+            self.flat.load_master(self.client_master[self.local_clients[0]])
+        ge = self._eval_global(r) if cfg.eval_global else None
+        loc = []
+        for c, t in local_eval.items():
+            a = t.cpu().tolist()
+            e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+            loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
+        client_metrics = [x for part in D.all_gather_object(loc) for x in part] if cfg.eval_local else []
+        if self.verbose and cfg.reference_prints:
+            for c, _, m in sorted(client_metrics):
+                print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
+        train_loss = self._reduce_train_loss(losses)
+        self._ledger_round(r, recs, {"kind": "mix", "rejected": sorted(v.rejected),
+                                     "stale_rounds": info.get("stale_rounds", 0.0)})
+        agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
+        return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
+                "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
+                "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
+                "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0)}
+
+    def _chain_round(self, r: int) -> dict:
+        """Reference C14 exactly: clients train one after another on ONE shared model; the
+        round ends with the unweighted mean of the K snapshots."""
+        snaps = torch.zeros_like(self.flat.master)
+        client_metrics, losses = [], {}
+        for c in self.local_clients:
+            self.opt.reset()
+            ops.rng.global_rng().load_state(self.client_rng[c])
+            losses[c] = self._train_client(c, r)
+            self.client_rng[c] = ops.rng.global_rng().state()
+            ops.weighted_accumulate_(snaps, self.flat.master, 1.0 / len(self.local_clients))
+            e = self.trainer.evaluate(self.test_batches(c, r))
+            client_metrics.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss}))
+            if self.verbose and self.cfg.reference_prints:
+                print("local_accuracy" + " :" + str(e.accuracy), flush=True)
+        self.flat.load_master(snaps)
+        ge = self._eval_global(r)
+        return {"distributed_accuracy": weighted_average([(n, m) for _, n, m in client_metrics]).get("accuracy"),
+                "global": ge, "train_loss": self._reduce_train_loss(losses), "rejected": [],
+                "client_metrics": client_metrics, "bytes_sent": 0.0}
+
+    # ================================ driver ====================================================
+    def run_round(self, r: int) -> dict:
+        t0 = time.perf_counter()
+        res = self.server_round(r) if self.cfg.mode == "server" else self.serverless_round(r)
+        self._maybe_save(r)
+        t_round = time.perf_counter() - t0
+        ge: Optional[EvalResult] = res.get("global")
+        gacc = ge.accuracy if ge is not None else None
+        if gacc is not None:
+            self.global_accuracies.append(gacc)
+            if self.verbose and self.cfg.reference_prints:
+                print(f"Global Model Accuracy: {gacc * 100:.2f}%", flush=True)
+        rec = {"round": r, "mode": self.cfg.mode, "t_round": t_round, "global_acc": gacc,
+               "global_loss": ge.loss if ge is not None else None,
+               "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
+               "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
+               "ledger_height": len(self.ledger) if self.ledger else 0,
+               "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
+        if self.is_cuda:
+            rec["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.device) / 1024 ** 3
+        for c, n_, m in res.get("client_metrics", []):
+            self.metrics.write({"round": r, "client": c, "local_acc": m.get("accuracy"),
+                                "local_loss": m.get("loss"), "examples": n_})
+        self.metrics.write(rec)
+        self.history.append(rec)
+        return rec
+
+    def _maybe_save(self, r: int):
+        cfg = self.cfg
+        if self.ckpt is None or (r + 1) % cfg.save_every:
+            return
+        with self.timer.phase("ckpt"):
+            state = {"round": r, "rng": ops.rng.global_rng().state(),
+                     "ledger_tip": self.ledger.tip if self.ledger else None,
+                     "global_accuracies": self.global_accuracies, "config": cfg.to_dict()}
+            dirs = []
+            if self.rt.is_main:
+                dirs.append(os.path.join(cfg.out_dir, "global"))
+            if cfg.save_clients and self.local_clients:
+                dirs.append(os.path.join(cfg.out_dir, f"client_{self.local_clients[0]}"))
+            src = self.global_master if cfg.mode == "server" else self.flat.master
+            self.ckpt.save(dirs, master=src, metadata={"round": str(r)}, state=state)
+
+    def run(self, rounds: Optional[int] = None) -> List[dict]:
+        cfg = self.cfg
+        end = cfg.num_rounds if rounds is None else self.start_round + rounds
+        for r in range(self.start_round, end):
+            self.run_round(r)
+        self.finish()
+        return self.history
+
+    def drain(self):
+        """Complete all in-flight communication (async gossip) and I/O."""
+        if self.gossip is not None:
+            self.gossip.drain()
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+    def finish(self):
+        self.drain()
+        if self.ckpt is not None:
+            self.ckpt.close()
+            if self.rt.is_main and self.cfg.compat_save_path and self.ckpt.last_dir:
+                mirror_dir(self.ckpt.last_dir, self.cfg.compat_save_path)
+        if self.ledger is not None:
+            bad = self.ledger.verify()
+            if bad != -1:
+                raise RuntimeError(f"ledger verification failed at height {bad}")
+        tel = self.telemetry.finish()
+        if self.verbose and self.cfg.reference_prints:
+            gdir = os.path.join(self.cfg.out_dir, "global")
+            size = dir_size_gb(gdir) if os.path.isdir(gdir) else None
+            Telemetry.print_reference_lines(tel, self.global_accuracies, size)
+        self.metrics.write({"final": True, **tel, "global_accuracies": self.global_accuracies})
+        self.metrics.close()
+        return tel
+
+    def _resume(self, path: str):
+        st_path = os.path.join(path, "global", "state.json")
+        if not os.path.exists(st_path):
+            raise FileNotFoundError(st_path)
+        with open(st_path) as fh:
+            st = json.load(fh)
+        load_into(self.model, self.flat, os.path.join(path, "global"))
+        if self.global_master is not None:
+            self.global_master.copy_(self.flat.master)
+        for c in self.client_master:
+            self.client_master[c].copy_(self.flat.master)
+        if self.gossip is not None:
+            self.gossip.seed_replicas(self.flat.master)
+        self.start_round = int(st["round"]) + 1
+        self.global_accuracies = list(st.get("global_accuracies", []))
+        led = os.path.join(path, "ledger.jsonl")
+        if self.ledger is not None and os.path.exists(led):
+            old = Ledger.load(led)
+            if old.verify() != -1:
+                raise RuntimeError("ledger in resume dir fails verification")
+            self.ledger = old
+            self.ledger.path = led if self.rt.is_main else None

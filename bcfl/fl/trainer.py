@@ -1,0 +1,82 @@
+"""Local training / evaluation on device (reference ``train()``/``test()``,
+``src/Servercase/server_IID_IMDB.py:108-135``, and ``IMDBClient.train_model``/``evaluate_model``,
+``src/Serverlesscase/serverless_IID_IMDB.py:156-187``).
+
+Differences by design: batches are packed and pre-staged on the device (one H2D per client per
+epoch instead of one per batch), the optimizer is the fused flat AdamW, and metrics accumulate
+on the device so an epoch has exactly one host sync.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Sequence
+
+import torch
+
+from .. import ops
+from ..data.batching import PackedBatch
+from ..parallel.flat import FlatAdamW, FlatParams
+
+
+@dataclass
+class EvalResult:
+    correct: int
+    count: int
+    loss_sum: float        # sum over examples of per-example CE
+    batch_mean_sum: float  # reference quirk: sum of per-batch mean losses
+
+    @property
+    def accuracy(self) -> float:
+        return self.correct / max(self.count, 1)
+
+    @property
+    def loss(self) -> float:
+        return self.loss_sum / max(self.count, 1)
+
+    @property
+    def ref_loss(self) -> float:
+        """Reference ``test()``: Σ batch-mean losses ÷ dataset size."""
+        return self.batch_mean_sum / max(self.count, 1)
+
+
+class LocalTrainer:
+    def __init__(self, model, flat: FlatParams, opt: FlatAdamW):
+        self.model, self.flat, self.opt = model, flat, opt
+
+    def train_epoch(self, batches: Sequence[PackedBatch]) -> Dict[str, torch.Tensor]:
+        m = self.model
+        m.train()
+        dev = self.flat.device
+        loss_acc = torch.zeros((), dtype=torch.float32, device=dev)
+        tokens = 0
+        for b in batches:
+            logits = m(b)
+            loss = ops.cross_entropy(logits, b.labels)
+            loss.backward()
+            self.opt.step()
+            self.flat.zero_grad()
+            loss_acc += loss.detach()
+            tokens += b.num_tokens
+        return {"loss_sum": loss_acc, "batches": len(batches), "tokens": tokens,
+                "examples": sum(b.batch_size for b in batches)}
+
+    @torch.no_grad()
+    def evaluate_device(self, batches: Sequence[PackedBatch]) -> torch.Tensor:
+        """[correct, count, loss_sum, batch_mean_sum] as a device fp64 tensor (no host sync)."""
+        m = self.model
+        m.eval()
+        dev = self.flat.device
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        for b in batches:
+            logits = m(b).float()
+            lab = b.labels.long()
+            ce = torch.nn.functional.cross_entropy(logits, lab, reduction="sum")
+            acc[0] += (logits.argmax(-1) == lab).sum()
+            acc[1] += b.batch_size
+            acc[2] += ce
+            acc[3] += ce / b.batch_size
+        return acc
+
+    def evaluate(self, batches: Sequence[PackedBatch]) -> EvalResult:
+        a = self.evaluate_device(batches).cpu().tolist()
+        return EvalResult(int(a[0]), int(a[1]), a[2], a[3])

@@ -1,0 +1,60 @@
+"""Loader for the in-tree native extension ``bcfl/_C*.so`` (HIP/CDNA4 kernels + bindings).
+
+Policy: a CUDA(HIP) tensor reaching a bcfl op REQUIRES the native extension — there is no
+silent eager fallback on the GPU path. CPU tensors use the PyTorch reference implementations in
+:mod:`bcfl.ops.ref` (the same math; used by the CPU test-suite and as numerics oracles).
+``BCFL_FORCE_TORCH=1`` routes GPU tensors to the reference path too (A/B benchmarking only).
+"""
+from __future__ import annotations
+
+import glob
+import importlib
+import os
+import sys
+
+_C = None
+_ERR = None
+
+
+def _load():
+    global _C, _ERR
+    if _C is not None or _ERR is not None:
+        return _C
+    pkg_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cands = glob.glob(os.path.join(pkg_dir, "_C*.so"))
+    if not cands:
+        _ERR = "bcfl/_C*.so not found (build it: python -m bcfl.csrc.build)"
+        return None
+    try:
+        import torch  # noqa: F401  (loads libtorch / libamdhip64 first)
+        _C = importlib.import_module("bcfl._C")
+    except Exception as e:  # pragma: no cover - depends on the build
+        _ERR = f"failed to import bcfl._C: {e!r}"
+        _C = None
+    return _C
+
+
+def native():
+    """Return the extension module or raise (GPU path must never silently fall back)."""
+    m = _load()
+    if m is None:
+        raise RuntimeError("bcfl native extension unavailable on a GPU code path: " + str(_ERR))
+    return m
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def force_torch() -> bool:
+    return os.environ.get("BCFL_FORCE_TORCH", "0") == "1"
+
+
+def use_native(t) -> bool:
+    """True when tensor ``t`` must go through the HIP kernels."""
+    return bool(getattr(t, "is_cuda", False)) and not force_torch()
+
+
+def load_error():
+    _load()
+    return _ERR

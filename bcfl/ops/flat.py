@@ -1,0 +1,127 @@
+"""Flat-buffer ops: fused AdamW (K10), FedAvg/gossip mixing (K11), sketches and SHA-256 Merkle.
+
+Every federated exchange in bcfl works on ONE contiguous buffer per client (parameters are views
+into it), so each op here is a single kernel launch over the whole model instead
+of the reference's per-tensor Python loops (HF AdamW over 201 tensors; ``sum(param)/len(param)``
+over ``zip(*aggregated_params)`` at ``src/Serverlesscase/serverless_IID_IMDB.py:269``).
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ref
+from ._native import native, use_native
+
+LEAF_BYTES_DEFAULT = 1 << 16  # 64 KiB Merkle leaves
+
+
+def adamw_(master, grad, m, v, step: int, lr: float, beta1: float, beta2: float, eps: float,
+           weight_decay: float, mode: str = "hf", param_out: Optional[torch.Tensor] = None,
+           grad_scale: float = 1.0):
+    if use_native(master):
+        native().adamw(master, grad, m, v, param_out, float(lr), float(beta1), float(beta2),
+                       float(eps), float(weight_decay), int(step), 0 if mode == "hf" else 1,
+                       float(grad_scale))
+        return
+    ref.adamw_(master, grad, m, v, step, lr, beta1, beta2, eps, weight_decay, mode, param_out,
+               grad_scale)
+
+
+def gossip_mix_(master: torch.Tensor, neighbours: Sequence[torch.Tensor], self_w: float,
+                weights: Sequence[float], param_out: Optional[torch.Tensor] = None):
+    """master <- self_w * master + sum_j w_j * neighbour_j (fp32 accumulate; neighbours any dtype)."""
+    if use_native(master):
+        native().mix(master, list(neighbours), float(self_w), [float(w) for w in weights], param_out)
+        return
+    ref.gossip_mix_(master, neighbours, self_w, weights, param_out)
+
+
+def weighted_accumulate_(acc: torch.Tensor, x: torch.Tensor, w: float):
+    if use_native(acc):
+        native().axpby(acc, x, float(w), 1.0)
+        return
+    ref.weighted_accumulate_(acc, x, w)
+
+
+def axpby_(y: torch.Tensor, x: torch.Tensor, a: float, b: float):
+    """y <- a*x + b*y."""
+    if use_native(y):
+        native().axpby(y, x, float(a), float(b))
+        return
+    y.mul_(b).add_(x.to(y.dtype), alpha=a)
+
+
+def scale_(x: torch.Tensor, a: float):
+    if use_native(x):
+        native().axpby(x, x, 0.0, float(a))
+        return
+    x.mul_(a)
+
+
+def cast_copy_(dst: torch.Tensor, src: torch.Tensor):
+    if use_native(dst) and dst.dtype != src.dtype:
+        native().cast_copy(dst, src)
+        return
+    dst.copy_(src)
+
+
+def block_sketch(x: torch.Tensor, dim: int, seed: int = 0x5EED) -> torch.Tensor:
+    if use_native(x):
+        return native().block_sketch(x, int(dim), int(seed))
+    return ref.block_sketch(x, dim, seed)
+
+
+# ------------------------------- SHA-256 Merkle ----------------------------------------------
+
+def _np_bytes(buf: torch.Tensor) -> np.ndarray:
+    t = buf.detach().reshape(-1)
+    if t.is_cuda:
+        t = t.cpu()
+    return t.contiguous().view(torch.uint8).numpy()
+
+
+def _leaf_digests_host(b: np.ndarray, leaf: int) -> List[bytes]:
+    n = max(1, (b.size + leaf - 1) // leaf)
+    mv = memoryview(b)
+    return [hashlib.sha256(b"\x00" + mv[i * leaf:(i + 1) * leaf].tobytes()).digest()
+            for i in range(n)]
+
+
+def merkle_from_leaves(leaves: Sequence[bytes]) -> bytes:
+    level = list(leaves)
+    if not level:
+        return hashlib.sha256(b"").digest()
+    while len(level) > 1:
+        nxt = []
+        for i in range(0, len(level) - 1, 2):
+            nxt.append(hashlib.sha256(b"\x01" + level[i] + level[i + 1]).digest())
+        if len(level) % 2:
+            nxt.append(level[-1])
+        level = nxt
+    return level[0]
+
+
+def leaf_digests_sha256(buf: torch.Tensor, leaf_bytes: int = LEAF_BYTES_DEFAULT) -> torch.Tensor:
+    """[n_leaves, 32] uint8 SHA-256(0x00 || leaf) digests (GPU kernel on device buffers)."""
+    if use_native(buf):
+        return native().sha256_leaves(buf, int(leaf_bytes))
+    ds = _leaf_digests_host(_np_bytes(buf), leaf_bytes)
+    return torch.from_numpy(np.frombuffer(b"".join(ds), dtype=np.uint8).reshape(-1, 32).copy())
+
+
+def merkle_root_sha256(buf: torch.Tensor, leaf_bytes: int = LEAF_BYTES_DEFAULT) -> bytes:
+    """RFC-6962-style Merkle root over the raw bytes of ``buf``.
+
+    GPU: leaves AND inner levels hashed on device (``sha256_leaves`` + ``sha256_merkle``), only
+    the 32-byte root crosses to the host (a 433 MB host SHA-256 would
+    dominate a ms-scale round)."""
+    if use_native(buf):
+        C = native()
+        leaves = C.sha256_leaves(buf, int(leaf_bytes))
+        root = C.sha256_merkle(leaves)
+        return bytes(root.cpu().numpy().tobytes())
+    return merkle_from_leaves(_leaf_digests_host(_np_bytes(buf), leaf_bytes))

@@ -1,0 +1,257 @@
+"""Public bcfl ops: autograd Functions that run the HIP/CDNA4 kernels on GPU tensors.
+
+Dispatch rule (see :mod:`bcfl.ops._native`): CUDA(HIP) tensors -> ``bcfl._C`` kernels (raise if
+the extension is missing); CPU tensors -> :mod:`bcfl.ops.ref` (autograd through torch ops).
+
+Hot-path ops (SURVEY.md §2.6 device-op inventory K1–K11):
+  * :func:`bias_dropout_add_layernorm` — K2: LN(dropout(y + b) + residual), one wave64 per row
+  * :func:`bias_act`                   — K6: bias + GELU/gelu_new/ReLU/tanh epilogue
+  * :func:`varlen_attention`           — K4: flash attention on packed rows (MFMA, online softmax)
+  * :func:`embedding_layernorm`        — K1+K2: word+pos+type gather, sum, LN, dropout
+  * :func:`rmsnorm`, :func:`rope_`, :func:`swiglu` — Llama path
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import ref
+from . import rng as _rng
+from ._native import native, use_native
+
+__all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
+           "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear"]
+
+
+def _keys(p: float, training: bool):
+    p8 = _rng.quantize_p(p) if (training and p > 0) else 0
+    ka, kb = _rng.global_rng().next() if p8 else (0, 0)
+    return p8, ka, kb
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Plain library GEMM (hipBLASLt via torch) — fused epilogues live in the following op."""
+    return torch.nn.functional.linear(x, w, b)
+
+
+# ----------------------------------------------------------------------------------------
+# K2: bias + dropout + residual + LayerNorm
+# ----------------------------------------------------------------------------------------
+class _BDALN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, bias, residual, gamma, beta, eps, p8, ka, kb):
+        C = native()
+        out, z, mean, rstd = C.bdaln_fwd(y, bias, residual, gamma, beta, float(eps), int(p8),
+                                         int(ka), int(kb))
+        ctx.save_for_backward(z, mean, rstd, gamma)
+        ctx.cfg = (p8, ka, kb, bias is not None, residual is not None, beta is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        z, mean, rstd, gamma = ctx.saved_tensors
+        p8, ka, kb, has_b, has_r, has_beta = ctx.cfg
+        dy, dbias, dres, dgamma, dbeta = native().bdaln_bwd(dout.contiguous(), z, mean, rstd,
+                                                            gamma, int(p8), int(ka), int(kb),
+                                                            bool(has_b))
+        return (dy, dbias if has_b else None, dres if has_r else None, dgamma,
+                dbeta if has_beta else None, None, None, None, None)
+
+
+def bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps: float, p: float = 0.0,
+                               training: bool = False):
+    p8, ka, kb = _keys(p, training)
+    if use_native(y):
+        return _BDALN.apply(y.contiguous(), bias, residual, gamma, beta, eps, p8, ka, kb)
+    return ref.bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps, p8, ka, kb)
+
+
+def layernorm(x, gamma, beta, eps: float):
+    return bias_dropout_add_layernorm(x, None, None, gamma, beta, eps, 0.0, False)
+
+
+# ----------------------------------------------------------------------------------------
+# K6: bias + activation
+# ----------------------------------------------------------------------------------------
+_ACT_ID = {"gelu": 0, "gelu_new": 1, "gelu_tanh": 1, "relu": 2, "tanh": 3, "silu": 4}
+
+
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, bias, act_id):
+        out = native().bias_act_fwd(y, bias, int(act_id))
+        ctx.save_for_backward(y, bias)
+        ctx.act_id = act_id
+        ctx.has_b = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, bias = ctx.saved_tensors
+        dy, dbias = native().bias_act_bwd(dout.contiguous(), y, bias, int(ctx.act_id))
+        return dy, (dbias if ctx.has_b else None), None
+
+
+def bias_act(y, bias, act: str = "gelu"):
+    if use_native(y):
+        return _BiasAct.apply(y.contiguous(), bias, _ACT_ID[act])
+    return ref.bias_act(y, bias, act)
+
+
+# ----------------------------------------------------------------------------------------
+# K4: varlen flash attention on a packed qkv projection
+# ----------------------------------------------------------------------------------------
+class _VarlenAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cu, max_s, nh, nkv, d, scale, causal, p8, ka, kb):
+        C = native()
+        out, lse = C.attn_fwd(qkv, cu, int(max_s), int(nh), int(nkv), int(d), float(scale),
+                              bool(causal), int(p8), int(ka), int(kb))
+        ctx.save_for_backward(qkv, cu, out, lse)
+        ctx.cfg = (max_s, nh, nkv, d, scale, causal, p8, ka, kb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, cu, out, lse = ctx.saved_tensors
+        max_s, nh, nkv, d, scale, causal, p8, ka, kb = ctx.cfg
+        dqkv = native().attn_bwd(dout.contiguous(), qkv, out, lse, cu, int(max_s), int(nh),
+                                 int(nkv), int(d), float(scale), bool(causal), int(p8), int(ka),
+                                 int(kb))
+        return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+def varlen_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, cu_host: Sequence[int],
+                     max_seqlen: int, num_heads: int, num_kv_heads: int, head_dim: int,
+                     dropout_p: float = 0.0, training: bool = False, causal: bool = False,
+                     scale: Optional[float] = None) -> torch.Tensor:
+    """qkv: [T, (nh + 2 nkv) * d] (q | k | v column blocks). Returns [T, nh * d]."""
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    p8, ka, kb = _keys(dropout_p, training)
+    if use_native(qkv):
+        return _VarlenAttn.apply(qkv.contiguous(), cu_seqlens, max_seqlen, num_heads,
+                                 num_kv_heads, head_dim, scale, causal, p8, ka, kb)
+    return ref.varlen_attention(qkv, num_heads, num_kv_heads, head_dim, cu_host, scale, causal,
+                                p8, ka, kb)
+
+
+# ----------------------------------------------------------------------------------------
+# K1 (+K2): embeddings gather-sum + LayerNorm + dropout
+# ----------------------------------------------------------------------------------------
+class _EmbLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8, ka, kb):
+        C = native()
+        out, z, mean, rstd = C.emb_ln_fwd(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma,
+                                          beta, float(eps), int(p8), int(ka), int(kb))
+        ctx.save_for_backward(ids, pos_ids, type_ids, z, mean, rstd, gamma, word_w, pos_w, type_w)
+        ctx.cfg = (p8, ka, kb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, pos_ids, type_ids, z, mean, rstd, gamma, word_w, pos_w, type_w = ctx.saved_tensors
+        p8, ka, kb = ctx.cfg
+        C = native()
+        dword, dpos, dtype_, dgamma, dbeta = C.emb_ln_bwd(
+            dout.contiguous(), ids, pos_ids, type_ids, z, mean, rstd, gamma, int(word_w.shape[0]),
+            int(pos_w.shape[0]) if pos_w is not None else 0,
+            int(type_w.shape[0]) if type_w is not None else 0, int(p8), int(ka), int(kb))
+        return (None, None, None, dword.to(word_w.dtype),
+                dpos.to(pos_w.dtype) if pos_w is not None else None,
+                dtype_.to(type_w.dtype) if type_w is not None else None,
+                dgamma, dbeta, None, None, None, None)
+
+
+def embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps: float,
+                        p: float = 0.0, training: bool = False):
+    p8, ka, kb = _keys(p, training)
+    if use_native(word_w):
+        return _EmbLN.apply(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8,
+                            ka, kb)
+    return ref.embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta,
+                                   eps, p8, ka, kb)
+
+
+# ----------------------------------------------------------------------------------------
+# Llama path: RMSNorm, RoPE, SwiGLU
+# ----------------------------------------------------------------------------------------
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        out, rstd = native().rmsnorm_fwd(x, w, float(eps))
+        ctx.save_for_backward(x, w, rstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = native().rmsnorm_bwd(dout.contiguous(), x, w, rstd, bool(w.requires_grad))
+        return dx, (dw if w.requires_grad else None), None
+
+
+def rmsnorm(x, w, eps: float):
+    if use_native(x):
+        return _RMSNorm.apply(x.contiguous(), w, eps)
+    return ref.rmsnorm(x, w, eps)
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, pos_ids, cos, sin, nrot_heads, d):
+        out = native().rope_fwd(qkv, pos_ids, cos, sin, int(nrot_heads), int(d), False)
+        ctx.save_for_backward(pos_ids, cos, sin)
+        ctx.cfg = (nrot_heads, d)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pos_ids, cos, sin = ctx.saved_tensors
+        nrot, d = ctx.cfg
+        dq = native().rope_fwd(dout.contiguous(), pos_ids, cos, sin, int(nrot), int(d), True)
+        return dq, None, None, None, None, None
+
+
+def rope(qkv: torch.Tensor, pos_ids, cos, sin, num_heads: int, num_kv_heads: int, head_dim: int):
+    """Rotate the q and k column blocks of a packed [T, (nh+2nkv)*d] projection (v untouched)."""
+    nrot = num_heads + num_kv_heads
+    if use_native(qkv):
+        return _Rope.apply(qkv.contiguous(), pos_ids, cos, sin, nrot, head_dim)
+    T = qkv.shape[0]
+    qk = qkv[:, : nrot * head_dim].reshape(T, nrot, head_dim)
+    qk = ref.rope(qk, pos_ids, cos, sin).reshape(T, nrot * head_dim)
+    return torch.cat([qk, qkv[:, nrot * head_dim:]], dim=1)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        return native().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        return native().swiglu_bwd(dout.contiguous(), gu)
+
+
+def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
+    if use_native(gate_up):
+        return _SwiGLU.apply(gate_up.contiguous())
+    return ref.swiglu(gate_up)
+
+
+def cross_entropy(logits, labels):
+    return torch.nn.functional.cross_entropy(logits.float(), labels.long())
+
+
+def dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
+    """Dropout on small head tensors ([B, H] pooler output) with the counter-based hash RNG, so
+    results are reproducible across processes (torch's global RNG is per process)."""
+    p8, ka, kb = _keys(p, training)
+    if p8 == 0:
+        return x
+    keep = _rng.keep_mask(x.numel(), p8, ka, kb, device=x.device).view_as(x)
+    return x * keep.to(x.dtype) * _rng.keep_scale(p8)

@@ -1,0 +1,130 @@
+"""One contiguous buffer per client: parameters, fp32 master, gradients and AdamW state.
+
+The reference serialises the model as 201 separate numpy arrays on every exchange
+(``get_parameters`` -> ``[val.cpu().numpy() for ...]``, ``src/Servercase/server_IID_IMDB.py:161-162``)
+and loads them back with ``torch.Tensor(v)`` + ``load_state_dict`` (``:164-167``). Here every
+trainable parameter is a VIEW into one flat device buffer (each tensor start aligned to 64
+elements = 128 B for bf16), so FedAvg is one RCCL all-reduce, a gossip exchange is one
+send/recv per peer, AdamW is one kernel, and host round-trips disappear (K12).
+
+Buffers (N = padded element count):
+  ``param``  compute dtype (bf16 on MI355X) — what the model reads
+  ``master`` fp32 master weights (aliases ``param`` when the compute dtype is fp32)
+  ``grad``   compute dtype; each ``p.grad`` is a view so autograd accumulates in place
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+ALIGN = 64
+
+
+class FlatParams:
+    def __init__(self, params: List[nn.Parameter], device=None, dtype: Optional[torch.dtype] = None,
+                 names: Optional[List[str]] = None):
+        if not params:
+            raise ValueError("no trainable parameters")
+        device = torch.device(device) if device is not None else params[0].device
+        dtype = dtype or params[0].dtype
+        self.device, self.dtype = device, dtype
+        self.names = names or [f"p{i}" for i in range(len(params))]
+        self.slots: List[Tuple[int, int, torch.Size]] = []
+        off = 0
+        for p in params:
+            n = p.numel()
+            self.slots.append((off, n, p.shape))
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.num_params = sum(n for _, n, _ in self.slots)
+        self.param = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=device)
+        with torch.no_grad():
+            for p, (o, n, shp) in zip(params, self.slots):
+                self.param[o:o + n].copy_(p.data.reshape(-1).to(device=device, dtype=dtype))
+        if dtype == torch.float32:
+            self.master = self.param
+        else:
+            self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
+            with torch.no_grad():
+                for p, (o, n, shp) in zip(params, self.slots):
+                    self.master[o:o + n].copy_(p.data.reshape(-1).to(device=device, dtype=torch.float32))
+        self.params = params
+        self._bind()
+
+    def _bind(self):
+        for p, (o, n, shp) in zip(self.params, self.slots):
+            p.data = self.param[o:o + n].view(shp)
+            p.grad = self.grad[o:o + n].view(shp)
+
+    @classmethod
+    def from_model(cls, model: nn.Module, device=None, dtype=None) -> "FlatParams":
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        return cls([p for _, p in named], device, dtype, [n for n, _ in named])
+
+    # ------------------------------------------------------------------------------------
+    def zero_grad(self):
+        self.grad.zero_()
+        for p, (o, n, shp) in zip(self.params, self.slots):  # autograd may have replaced .grad
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
+                p.grad = self.grad[o:o + n].view(shp)
+
+    @torch.no_grad()
+    def sync_param_from_master(self):
+        if self.master is not self.param:
+            ops.cast_copy_(self.param, self.master)
+
+    @torch.no_grad()
+    def load_master(self, src: torch.Tensor):
+        self.master.copy_(src)
+        self.sync_param_from_master()
+
+    def nbytes(self, which: str = "param") -> int:
+        t = getattr(self, which)
+        return t.numel() * t.element_size()
+
+    def state_views(self, buf: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        buf = self.master if buf is None else buf
+        return {nm: buf[o:o + n].view(shp) for nm, (o, n, shp) in zip(self.names, self.slots)}
+
+
+class FlatAdamW:
+    """Fused AdamW over a FlatParams (ONE kernel per step; K10).
+
+    ``mode="hf"`` reproduces ``transformers.AdamW`` (4.35: eps outside the bias correction,
+    ``correct_bias=True``) that the reference instantiates at ``server_IID_IMDB.py:109``;
+    ``mode="torch"`` reproduces ``torch.optim.AdamW``. ``reset()`` = the reference's fresh
+    optimizer per fit (C8)."""
+
+    def __init__(self, flat: FlatParams, lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-6,
+                 weight_decay: float = 0.0, mode: str = "hf"):
+        self.flat = flat
+        self.lr, self.betas, self.eps, self.wd, self.mode = lr, tuple(betas), eps, weight_decay, mode
+        self.m = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+        self.v = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+        self.step_count = 0
+
+    def reset(self):
+        self.m.zero_()
+        self.v.zero_()
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0):
+        self.step_count += 1
+        f = self.flat
+        ops.adamw_(f.master, f.grad, self.m, self.v, self.step_count, self.lr, self.betas[0],
+                   self.betas[1], self.eps, self.wd, self.mode,
+                   param_out=None if f.master is f.param else f.param, grad_scale=grad_scale)
+
+    def state_dict(self):
+        return {"m": self.m, "v": self.v, "step": self.step_count}
+
+    def load_state_dict(self, st):
+        self.m.copy_(st["m"])
+        self.v.copy_(st["v"])
+        self.step_count = int(st["step"])

@@ -1,0 +1,122 @@
+#!/usr/bin/env python
+"""Headline benchmark: per-round wall-clock (+ final accuracy) of BERT-base, 8-client async P2P
+gossip, Non-IID — BASELINE.json's metric on BASELINE.json config 3.
+
+One "step" = one federated ROUND of an 8-client federation: every client trains one local epoch
+(240 samples = 8 batches of 32, reference ``serverless_NonIID_IMDB.py:59``), evaluates on its 60
+local test rows, publishes its model over RCCL send/recv (async, overlapped with the next round),
+mixes its neighbours' models, the federation evaluates the global model on a 100-row draw, every
+client update is Merkle-hashed into the ledger, and the global model is checkpointed (async).
+
+Scaling: the federation always has 8 clients (the config names 8); N GPUs host 8/N clients each
+(strong scaling over GPUs). ``value`` = seconds per round for the whole job (max over ranks).
+
+    python bench.py                                   # 1 GPU, 8 virtual clients
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# reference serverless IMDB latency (All_graphs_IMDB_dataset.ipynb:748): 27.8 min @5 workers,
+# 40 min @10 workers over 20 rounds -> 1.39 / 2.00 min/round; linear interpolation at 8 clients:
+BASELINE_S_PER_ROUND = (27.8 + (40.0 - 27.8) * (8 - 5) / (10 - 5)) / 20.0 * 60.0  # 105.36 s
+# reference final global accuracy, serverless Non-IID IMDB (All_graphs_IMDB_dataset.ipynb:1142)
+BASELINE_FINAL_ACC = 0.54
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="bert-base")
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--mode", default="serverless")
+    ap.add_argument("--lr", type=float, default=5e-5)
+    ap.add_argument("--sync", action="store_true", help="synchronous gossip instead of async")
+    ap.add_argument("--no-ledger", action="store_true")
+    ap.add_argument("--no-ckpt", action="store_true")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--device", default="auto")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    from bcfl.config import get_preset
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+
+    rt = D.init_runtime(a.device)
+    out = a.out or os.path.join("runs", "bench", f"n{rt.world}")
+    cfg = get_preset("baseline3_bert_serverless_noniid", model=a.model, num_clients=a.clients,
+                     num_rounds=a.warmup + a.steps, mode=a.mode, lr=a.lr,
+                     async_gossip=not a.sync, ledger=not a.no_ledger,
+                     save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
+                     device=a.device)
+    fed = Federation(cfg, verbose=False)
+    for r in range(a.warmup):
+        fed.run_round(r)
+    fed.drain()
+    D.barrier()
+    if fed.is_cuda:
+        torch.cuda.synchronize()
+    tok0 = fed.tokens_trained
+    t0 = time.perf_counter()
+    for r in range(a.warmup, a.warmup + a.steps):
+        fed.run_round(r)
+    fed.drain()  # the last async exchange is part of the timed work
+    D.barrier()
+    if fed.is_cuda:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = D.max_over_ranks(dt)
+    tokens = float(fed.tokens_trained - tok0)
+    tok_t = torch.tensor([tokens], dtype=torch.float64, device=fed.device)
+    D.all_reduce_(tok_t)
+    tokens = float(tok_t.item())
+    final_acc = fed.global_accuracies[-1] if fed.global_accuracies else None
+    s_per_round = dt / a.steps
+    phases = {k: v for k, v in fed.history[-1].items() if k.startswith("t_")}
+    fed.finish()
+    if rt.is_main:
+        rec = {
+            "metric": "per-round wall-clock + final accuracy, BERT-base 8-client async P2P Non-IID",
+            "value": s_per_round,
+            "unit": "s/round",
+            "n_gpus": rt.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": s_per_round * 1000.0,
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": s_per_round / BASELINE_S_PER_ROUND,
+            "speedup_vs_baseline": BASELINE_S_PER_ROUND / s_per_round,
+            "baseline_s_per_round": BASELINE_S_PER_ROUND,
+            "final_accuracy": final_acc,
+            "baseline_final_accuracy": BASELINE_FINAL_ACC,
+            "accuracy_note": "synthetic IMDB-shaped data + random-init weights; not comparable to pretrained accuracy on real IMDB",
+            "tokens_per_s": tokens / dt,
+            "samples_per_s": a.clients * cfg.train_samples * a.steps / dt,
+            "dtype": "bf16",
+            "data": "synthetic (IMDB-shaped lengths, label-sorted Non-IID shards, packed varlen); random-init weights",
+            "config": {"model": a.model, "global_batch": 32 * a.clients, "seq_len": 512,
+                       "parallelism": f"fl{a.clients}-clients-on-{rt.world}gpu",
+                       "clients": a.clients, "mode": a.mode,
+                       "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
+                       "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
+                       "checkpoint_every_round": cfg.save_every == 1},
+            "last_round_phases_s": phases,
+        }
+        print(json.dumps(rec), flush=True)
+    D.shutdown()
+
+
+if __name__ == "__main__":
+    main()

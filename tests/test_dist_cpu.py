@@ -1,0 +1,108 @@
+"""Multi-process (gloo, world 2) tests of the distributed paths — the CPU stand-in for the 8-GPU
+node. Key property: N real ranks give BIT-IDENTICAL models to 1 rank hosting N virtual clients."""
+import os
+
+import pytest
+import torch
+
+from dist_utils import run_world
+
+
+def _cfg(mode, out, **kw):
+    from bcfl.config import FLConfig
+    base = dict(mode=mode, model="tiny-bert", dataset="tiny", num_clients=2, num_rounds=2,
+                train_samples=48, test_samples=16, global_test_samples=32, batch_size=16, lr=1e-3,
+                out_dir=out, partition="label_shards", reference_prints=False, save_every=0,
+                device="cpu", backend="gloo")
+    base.update(kw)
+    return FLConfig(**base)
+
+
+def _fed_worker(rank, world, mode, out, kw):
+    from bcfl.fl import Federation
+    fed = Federation(_cfg(mode, out, **kw), verbose=False)
+    fed.run()
+    res = {"master": fed.flat.master.clone(), "acc": torch.tensor(fed.global_accuracies)}
+    if fed.ledger is not None:
+        res["tip"] = fed.ledger.tip
+        res["consensus"] = fed.ledger.consensus_check()
+    return res
+
+
+def _single(mode, out, **kw):
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(2)  # same intra-op threading as the workers -> same reduction order
+    try:
+        fed = Federation(_cfg(mode, out, **kw), verbose=False)
+        fed.run()
+    finally:
+        torch.set_num_threads(nt)
+    m = fed.flat.master.clone()
+    D.set_runtime_for_tests(None)
+    return m, fed
+
+
+def test_p2p_exchange(tmp_path):
+    res = run_world(_p2p_worker, 2, str(tmp_path))
+    assert torch.equal(res[0], torch.arange(1000, dtype=torch.float32) + 1000)
+    assert torch.equal(res[1], torch.arange(1000, dtype=torch.float32))
+
+
+def _p2p_worker(rank, world):
+    from bcfl.parallel import dist as D
+    D.init_runtime("cpu", "gloo")
+    send = torch.arange(1000, dtype=torch.float32) + 1000 * rank
+    recv = torch.empty(1000)
+    h = D.p2p_exchange([(send, 1 - rank)], [(recv, 1 - rank)])
+    h.wait()
+    return recv
+
+
+def test_server_fedavg_ranks_equal_virtual(tmp_path):
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), "server", str(tmp_path / "d"), {})
+    assert torch.equal(res[0]["master"], res[1]["master"])
+    single, _ = _single("server", str(tmp_path / "s"))
+    assert torch.equal(res[0]["master"], single)
+    assert res[0]["consensus"] and res[0]["tip"] == res[1]["tip"]
+
+
+def test_serverless_sync_ranks_equal_virtual(tmp_path):
+    # fp32 wire: full topology + average mixing = the reference's mean of snapshots; both clients
+    # end every round on the bit-identical model, and 2 ranks == 2 virtual clients on 1 rank
+    kw = {"async_gossip": False, "wire_dtype": "fp32"}
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
+    assert torch.equal(res[0]["master"], res[1]["master"])
+    single, fed = _single("serverless", str(tmp_path / "s"), **kw)
+    assert torch.equal(res[0]["master"], single)
+
+
+def test_serverless_bf16_delta_wire_close(tmp_path):
+    # bf16 error-feedback deltas: neighbours differ only by bf16 rounding of ONE round's delta
+    kw = {"async_gossip": False, "wire_dtype": "bf16", "num_rounds": 3}
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
+    diff = (res[0]["master"] - res[1]["master"]).abs().max().item()
+    assert diff < 1e-4
+    single, _ = _single("serverless", str(tmp_path / "s"), **kw)
+    assert torch.equal(res[0]["master"], single)
+
+
+def test_serverless_async_runs_and_mixes(tmp_path):
+    kw = {"async_gossip": True, "num_rounds": 3, "anomaly_filter": "both"}
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
+    a, b = res[0]["master"], res[1]["master"]
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    # mixing pulled the clients together relative to independent training
+    single, _ = _single("serverless", str(tmp_path / "s"), **kw)
+    torch.testing.assert_close(a, single, atol=1e-6, rtol=0)
+    assert res[0]["consensus"]
+
+
+def test_serverless_ring_four_ranks(tmp_path):
+    kw = {"num_clients": 4, "topology": "ring", "mixing": "metropolis", "async_gossip": False,
+          "wire_dtype": "fp32", "num_rounds": 2}
+    res = run_world(_fed_worker, 4, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
+    single, _ = _single("serverless", str(tmp_path / "s"), **kw)
+    torch.testing.assert_close(res[0]["master"], single, atol=1e-6, rtol=0)

@@ -1,0 +1,144 @@
+"""Single-process federation tests: rounds, reference quirks, checkpoints, resume, fault injection."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from bcfl.config import FLConfig
+from bcfl.fl import Client, Federation, weighted_average
+from bcfl.parallel import dist as D
+
+
+def _cfg(out, **kw):
+    base = dict(model="tiny-bert", dataset="tiny", num_clients=3, num_rounds=2, train_samples=48,
+                test_samples=16, global_test_samples=32, batch_size=16, lr=1e-3, out_dir=out,
+                partition="label_shards", reference_prints=False, device="cpu", async_ckpt=False)
+    base.update(kw)
+    return FLConfig(**base)
+
+
+@pytest.fixture(autouse=True)
+def _fresh_runtime():
+    D.set_runtime_for_tests(None)
+    yield
+    D.set_runtime_for_tests(None)
+
+
+def test_weighted_average_reference_semantics():
+    m = weighted_average([(10, {"accuracy": 0.5, "loss": 1.0}), (30, {"accuracy": 0.9, "loss": 2.0})])
+    assert m["accuracy"] == pytest.approx(0.8) and m["loss"] == pytest.approx(1.75)
+
+
+def test_server_round_is_weighted_fedavg(tmp_out):
+    cfg = _cfg(tmp_out, mode="server", num_rounds=1, ledger=False, save_every=0,
+               partition="dirichlet", train_samples=40)
+    fed = Federation(cfg, verbose=False)
+    g0 = fed.global_master.clone()
+    # replay each client's local training by hand and average with Σ n_k w_k / Σ n
+    states, ns = [], []
+    for c in range(3):
+        fed._activate(c, master=g0)
+        fed._train_client(c, 0)
+        states.append(fed.flat.master.clone())
+        ns.append(fed.client_examples(c, 0))
+        fed._deactivate(c)
+    fed.flat.load_master(g0)
+    for c in range(3):
+        fed.client_rng[c] = {"seed": fed.client_rng[c]["seed"], "counter": 0}
+    fed.run_round(0)
+    w = np.array(ns, dtype=np.float64) / sum(ns)
+    expect = sum(float(w[i]) * states[i] for i in range(3))
+    torch.testing.assert_close(fed.global_master, expect, atol=1e-6, rtol=1e-5)
+
+
+def test_serverless_compat_chain(tmp_out):
+    cfg = _cfg(tmp_out, mode="serverless", compat_chain=True, ledger=False, save_every=0)
+    fed = Federation(cfg, verbose=False)
+    h = fed.run()
+    assert len(h) == 2 and all(0.0 <= r["global_acc"] <= 1.0 for r in h)
+
+
+def test_checkpoint_roundtrip_and_hf_load(tmp_out):
+    transformers = pytest.importorskip("transformers")
+    cfg = _cfg(tmp_out, mode="serverless", compat_save_path=os.path.join(tmp_out, "my_albert_model2"))
+    fed = Federation(cfg, verbose=False)
+    fed.run()
+    gdir = os.path.join(tmp_out, "global")
+    assert os.path.exists(os.path.join(gdir, "model.safetensors"))
+    assert os.path.exists(os.path.join(tmp_out, "my_albert_model2", "model.safetensors"))
+    from bcfl.ckpt import read_safetensors
+    sd = read_safetensors(os.path.join(gdir, "model.safetensors"))
+    assert len(sd) == len(fed.model.hf_state_dict())
+    hf = transformers.AutoModelForSequenceClassification.from_pretrained(gdir)
+    assert type(hf).__name__ == "BertForSequenceClassification"
+    ours = fed.model.hf_state_dict()
+    for k, v in hf.state_dict().items():
+        if k in ours:
+            torch.testing.assert_close(v, ours[k].float())
+    st = json.load(open(os.path.join(gdir, "state.json")))
+    assert st["round"] == 1
+    # ledger + metrics artefacts
+    rows = [json.loads(l) for l in open(os.path.join(tmp_out, "ledger.jsonl"))]
+    assert rows[0]["kind"] == "genesis" and len(rows) == 1 + 2 * (3 + 1)
+    mets = [json.loads(l) for l in open(os.path.join(tmp_out, "metrics.jsonl"))]
+    assert any("t_round" in m for m in mets) and mets[-1].get("final")
+
+
+def test_resume_continues_rounds(tmp_out):
+    cfg = _cfg(tmp_out, mode="server", num_rounds=2)
+    fed = Federation(cfg, verbose=False)
+    fed.run()
+    master = fed.global_master.clone()
+    fed2 = Federation(_cfg(tmp_out + "_r", mode="server", num_rounds=3, resume=tmp_out), verbose=False)
+    assert fed2.start_round == 2
+    torch.testing.assert_close(fed2.global_master, master)
+    h = fed2.run()
+    assert [r["round"] for r in h] == [2]
+
+
+def test_client_api_matches_reference_contract(tmp_out):
+    fed = Federation(_cfg(tmp_out, mode="server", ledger=False, save_every=0), verbose=False)
+    cl = Client(fed, 0)
+    params = cl.get_parameters({})
+    assert len(params) == len(fed.model.hf_state_dict())
+    new, n, met = cl.fit(params, {})
+    assert n == 48 and len(new) == len(params)
+    assert any(not np.array_equal(a, b) for a, b in zip(new, params))
+    loss, n_te, m = cl.evaluate(new, {})
+    assert n_te == 16 and 0.0 <= m["accuracy"] <= 1.0 and m["loss"] == loss
+    cl.set_parameters(params)
+    assert all(np.array_equal(a, b) for a, b in zip(cl.get_parameters(), params))
+
+
+def test_fault_injection_byzantine_rejected_and_recorded(tmp_out):
+    cfg = _cfg(tmp_out, mode="serverless", num_clients=6, num_rounds=2, partition="iid_random",
+               anomaly_filter="both", anomaly_k=1.5, inject_byzantine={4: -20.0},
+               async_gossip=False, save_every=0, train_samples=32)
+    fed = Federation(cfg, verbose=False)
+    h = fed.run()
+    assert all(4 in r["rejected"] for r in h)
+    blocks = fed.ledger.blocks()
+    v = [b["verdict"] for b in blocks if b["client"] == 4 and b["kind"] == "update"]
+    assert v and all(x.startswith("reject") for x in v)
+    assert fed.ledger.verify() == -1
+
+
+def test_fault_injection_slow_client(tmp_out):
+    cfg = _cfg(tmp_out, mode="server", num_rounds=1, inject_slow={1: 50.0}, ledger=False, save_every=0)
+    fed = Federation(cfg, verbose=False)
+    rec = fed.run()[0]
+    assert rec["t_round"] >= 0.05
+
+
+def test_llama_lora_federation_delta_only(tmp_out):
+    cfg = _cfg(tmp_out, model="tiny-llama-lora", mode="serverless", num_rounds=1, lr=1e-3)
+    fed = Federation(cfg, verbose=False)
+    n_train = sum(p.numel() for p in fed.model.parameters() if p.requires_grad)
+    n_all = sum(p.numel() for p in fed.model.parameters())
+    assert fed.flat.num_params == n_train < n_all / 4  # only adapters + head are exchanged
+    fed.run()
+    from bcfl.ckpt import read_safetensors
+    sd = read_safetensors(os.path.join(tmp_out, "global", "model.safetensors"))
+    assert all("lora_" in k or "score" in k for k in sd)

@@ -1,0 +1,126 @@
+"""Trust layer: golden outputs of the reference notebooks, native-vs-NumPy agreement, ledger."""
+import json
+
+import numpy as np
+import pytest
+
+from bcfl.trust import graph as G
+from bcfl.trust import netdata as nd
+from bcfl.trust.anomaly import UpdateAnomalyFilter, topology_filter
+from bcfl.trust.ledger import Ledger, block_hash
+
+
+@pytest.mark.parametrize("use_native", [True, False])
+def test_pagerank_golden(use_native):
+    if use_native and not G.native_available():
+        pytest.skip("host lib not built")
+    r = G.pagerank(nd.ref_weight_matrix(), use_native=use_native)
+    (lo, hi), flags = G.sigma_flags(r, 1.0)
+    assert lo == pytest.approx(nd.REF_PAGERANK_THRESHOLDS[0], abs=1e-12)
+    assert hi == pytest.approx(nd.REF_PAGERANK_THRESHOLDS[1], abs=1e-12)
+    assert flags == nd.REF_PAGERANK_ANOMALIES
+
+
+def test_pagerank_matches_networkx_random_graphs():
+    nx = pytest.importorskip("networkx")
+    rs = np.random.default_rng(0)
+    for n in (5, 12, 30):
+        W = rs.random((n, n)) * (rs.random((n, n)) < 0.5)
+        np.fill_diagonal(W, 0)
+        W[0] = 0  # a dangling node
+        Gx = nx.DiGraph()
+        Gx.add_nodes_from(range(n))
+        for i in range(n):
+            for j in range(n):
+                if W[i, j] > 0:
+                    Gx.add_edge(i, j, weight=W[i, j])
+        pr = nx.pagerank(Gx, weight="weight")
+        ours = G.pagerank(W)
+        assert np.allclose([pr[i] for i in range(n)], ours, atol=1e-12)
+
+
+def test_reference_detector_outputs():
+    rep = G.anomaly_report(nd.REF_BW_MBPS)
+    assert rep["pagerank"] == nd.REF_PAGERANK_ANOMALIES
+    assert rep["modz"] == nd.REF_MODZ_ANOMALIES
+    assert rep["dbscan"] == nd.REF_DBSCAN_ANOMALIES
+    assert rep["louvain"] == nd.REF_LOUVAIN_ANOMALIES
+
+
+def test_dbscan_matches_sklearn():
+    sk = pytest.importorskip("sklearn.cluster")
+    rs = np.random.default_rng(1)
+    X = np.concatenate([rs.normal(0, 0.3, (20, 2)), rs.normal(5, 0.3, (20, 2)), rs.uniform(-10, 10, (5, 2))])
+    ours = G.dbscan(X, 0.8, 4)
+    theirs = sk.DBSCAN(eps=0.8, min_samples=4).fit_predict(X)
+    assert ((ours == -1) == (theirs == -1)).all()
+
+
+def test_modified_z_and_native_agree():
+    v = list(np.random.default_rng(2).random(15))
+    z = G.modified_z(v)
+    med = np.median(v)
+    mad = np.median(np.abs(np.array(v) - med))
+    assert np.allclose(z, 0.6745 * (np.array(v) - med) / mad)
+
+
+def test_info_passing_and_best_source():
+    L = G.latency_matrix(nd.REF_BW_MBPS, nd.BIOBERT_GB * 8 * 1000)  # Gb -> Mb over Mbps = s
+    t_all = G.info_passing_time(L, 0)
+    assert t_all.reached == 9 and t_all.async_ <= t_all.sync
+    t_f = G.info_passing_time(L, 1, excluded=nd.REF_PAGERANK_ANOMALIES)
+    assert t_f.reached == 9 - 4
+    d = G.shortest_paths(L, 0)
+    assert d[0] == 0 and np.all(d[1:] <= L[0, 1:] + 1e-12)
+    s, obj = G.best_source(L, (), 1.0)
+    assert 0 <= s < 10 and obj >= 1.0
+    # async (max) beats sync (sum) by a wide margin: the paper's -76% claim is structural
+    assert t_all.async_ / t_all.sync < 0.24
+
+
+def test_topology_filter_uniform_links():
+    bw = np.full((8, 8), 150.0)
+    np.fill_diagonal(bw, 0)
+    assert topology_filter(bw) == []
+    bw[3, :] = bw[:, 3] = 15.0
+    bw[3, 3] = 0
+    assert 3 in topology_filter(bw, k=1.0)
+
+
+def test_update_filter_rejects_byzantine():
+    rs = np.random.default_rng(0)
+    base = rs.normal(size=4096)
+    sk = np.stack([base + 0.3 * rs.normal(size=4096) for _ in range(8)])
+    sk[5] = -sk[5]           # sign-flipped update
+    norms = [1.0] * 8
+    norms[2] = 50.0          # boosted update
+    v = UpdateAnomalyFilter("both", k=1.5)(sk, norms)
+    assert 5 in v.rejected and 2 in v.rejected
+    assert len(v.rejected) <= 3
+    assert v.verdict(5).startswith("reject") and v.verdict(0) == "accept"
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_ledger_chain(native, tmp_path):
+    if native and not G.native_available():
+        pytest.skip("host lib not built")
+    path = str(tmp_path / "ledger.jsonl")
+    L = Ledger({"x": 1}, path=path, native=native, ts=0.0)
+    for r in range(3):
+        for c in range(4):
+            b = L.append(r, c, "update", "ab" * 32, "accept", {"acc": 0.5 + c}, ts=r + c / 10)
+            assert b["height"] == len(L) - 1
+    assert L.verify() == -1
+    L.flush()
+    L2 = Ledger.load(path, native=native)
+    assert L2.tip == L.tip and L2.verify() == -1
+    L.tamper(5, "payload", json.dumps({"acc": 99}))
+    assert L.verify() == 5
+    # python and native chains hash identically
+    other = Ledger({"x": 1}, native=not native, ts=0.0)
+    for r in range(3):
+        for c in range(4):
+            other.append(r, c, "update", "ab" * 32, "accept", {"acc": 0.5 + c}, ts=r + c / 10)
+    assert other.tip == L2.tip
+    blk = L2.block(3)
+    assert block_hash(blk) == blk["hash"]
