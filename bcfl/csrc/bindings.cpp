@@ -1,0 +1,423 @@
+// torch bindings of the bcfl gfx950 kernels (module bcfl._C).
+//
+// Only tensor plumbing lives here: shape/dtype checks, output allocation on the caller's stream,
+// and a call into the raw-pointer launchers of csrc/kernels/*.hip. Every op runs on the current
+// HIP stream so it composes with torch's stream semantics (and RCCL's side streams).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "kernels/kernels.h"
+
+namespace {
+
+using torch::Tensor;
+using c10::optional;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dt_of(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return bcfl::DT_BF16;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "bcfl kernels support bf16 / fp32, got ", t.scalar_type());
+  return bcfl::DT_F32;
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+const void* ptr_or_null(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+
+void check_rc(int rc, const char* op) {
+  TORCH_CHECK(rc == 0, "bcfl kernel ", op, " rejected the shape (code ", rc, ")");
+  auto e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, "bcfl kernel ", op, " launch failed: ", hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------------------------------------
+std::vector<Tensor> bdaln_fwd(Tensor y, optional<Tensor> bias, optional<Tensor> res,
+                              optional<Tensor> gamma, optional<Tensor> beta, double eps, int64_t p8,
+                              int64_t ka, int64_t kb) {
+  check_cuda(y, "y");
+  const int H = y.size(-1);
+  const int T = y.numel() / H;
+  if (res.has_value() && res->defined()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->numel() == y.numel(), "residual shape");
+  }
+  auto out = torch::empty_like(y);
+  auto z = torch::empty_like(y);
+  auto f = y.options().dtype(torch::kFloat);
+  auto mean = torch::empty({T}, f), rstd = torch::empty({T}, f);
+  const int pdt = gamma.has_value() && gamma->defined() ? dt_of(*gamma) : dt_of(y);
+  TORCH_CHECK(pdt == dt_of(y), "LayerNorm params must share the activation dtype");
+  check_rc(bcfl::launch_bdaln_fwd(y.data_ptr(), ptr_or_null(bias), ptr_or_null(res),
+                                  ptr_or_null(gamma), ptr_or_null(beta), out.data_ptr(),
+                                  z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), T,
+                                  H, (float)eps, (uint32_t)p8, (uint32_t)ka, (uint32_t)kb, dt_of(y),
+                                  stream()),
+           "bdaln_fwd");
+  return {out, z, mean, rstd};
+}
+
+std::vector<Tensor> bdaln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd,
+                              optional<Tensor> gamma, int64_t p8, int64_t ka, int64_t kb,
+                              bool has_bias) {
+  check_cuda(dout, "dout");
+  check_cuda(z, "z");
+  const int H = z.size(-1);
+  const int T = z.numel() / H;
+  auto dz = torch::empty_like(z);
+  Tensor dy = p8 ? torch::empty_like(z) : dz;
+  const int nblk = bcfl::bwd_blocks(T);
+  auto f = z.options().dtype(torch::kFloat);
+  auto partial = torch::empty({nblk, 3, H}, f);
+  const int dt = dt_of(z);
+  check_rc(bcfl::launch_bdaln_bwd(dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(),
+                                  rstd.data_ptr<float>(), ptr_or_null(gamma), dz.data_ptr(),
+                                  p8 ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk, T,
+                                  H, (uint32_t)p8, (uint32_t)ka, (uint32_t)kb, has_bias ? 1 : 0,
+                                  dt, stream()),
+           "bdaln_bwd");
+  auto popt = z.options();
+  auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);
+  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 0, H, dgamma.data_ptr(), dt, stream()), "colsum");
+  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 1, H, dbeta.data_ptr(), dt, stream()), "colsum");
+  Tensor dbias;
+  if (has_bias) {
+    dbias = torch::empty({H}, popt);
+    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 2, H, dbias.data_ptr(), dt, stream()), "colsum");
+  }
+  return {dy, dbias, dz, dgamma, dbeta};
+}
+
+Tensor bias_act_fwd(Tensor y, optional<Tensor> bias, int64_t act) {
+  check_cuda(y, "y");
+  const int N = y.size(-1);
+  auto out = torch::empty_like(y);
+  check_rc(bcfl::launch_bias_act_fwd(y.data_ptr(), ptr_or_null(bias), out.data_ptr(),
+                                     y.numel() / N, N, (int)act, dt_of(y), stream()),
+           "bias_act_fwd");
+  return out;
+}
+
+std::vector<Tensor> bias_act_bwd(Tensor dout, Tensor y, optional<Tensor> bias, int64_t act) {
+  check_cuda(dout, "dout");
+  check_cuda(y, "y");
+  const int N = y.size(-1);
+  const int64_t rows = y.numel() / N;
+  auto dy = torch::empty_like(y);
+  const bool hb = bias.has_value() && bias->defined();
+  int nblk = (int)std::min<int64_t>(std::max<int64_t>(rows / 32, 1), 256);
+  Tensor partial;
+  if (hb) partial = torch::empty({nblk, N}, y.options().dtype(torch::kFloat));
+  check_rc(bcfl::launch_bias_act_bwd(dout.data_ptr(), y.data_ptr(), ptr_or_null(bias),
+                                     dy.data_ptr(), hb ? partial.data_ptr<float>() : nullptr, nblk,
+                                     rows, N, (int)act, dt_of(y), stream()),
+           "bias_act_bwd");
+  Tensor dbias;
+  if (hb) {
+    dbias = torch::empty({N}, bias->options());
+    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 1, 0, N, dbias.data_ptr(),
+                                 dt_of(*bias), stream()), "colsum");
+  }
+  return {dy, dbias};
+}
+
+// ------------------------------------------------------------------------------------------------
+std::vector<Tensor> attn_fwd(Tensor qkv, Tensor cu, int64_t max_s, int64_t nh, int64_t nkv,
+                             int64_t d, double scale, bool causal, int64_t p8, int64_t ka,
+                             int64_t kb) {
+  check_cuda(qkv, "qkv");
+  check_cuda(cu, "cu_seqlens");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "attention kernels take bf16");
+  TORCH_CHECK(cu.scalar_type() == at::kInt, "cu_seqlens must be int32");
+  TORCH_CHECK(qkv.size(-1) == (nh + 2 * nkv) * d, "qkv width != (nh + 2 nkv) * d");
+  TORCH_CHECK(max_s <= 8192, "max_seqlen > 8192 (dropout index stride)");
+  const int T = qkv.size(0);
+  auto out = torch::empty({T, nh * d}, qkv.options());
+  auto lse = torch::empty({T, nh}, qkv.options().dtype(torch::kFloat));
+  bcfl::AttnParams p{};
+  p.qkv = qkv.data_ptr();
+  p.out = out.data_ptr();
+  p.lse = lse.data_ptr<float>();
+  p.cu = cu.data_ptr<int>();
+  p.B = cu.numel() - 1;
+  p.T = T;
+  p.nh = nh; p.nkv = nkv; p.d = d; p.max_s = max_s;
+  p.scale = (float)scale;
+  p.causal = causal;
+  p.p8 = (uint32_t)p8; p.ka = (uint32_t)ka; p.kb = (uint32_t)kb;
+  if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_fwd(p, stream()), "attn_fwd");
+  return {out, lse};
+}
+
+Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int64_t max_s,
+                int64_t nh, int64_t nkv, int64_t d, double scale, bool causal, int64_t p8,
+                int64_t ka, int64_t kb) {
+  check_cuda(dout, "dout");
+  check_cuda(qkv, "qkv");
+  check_cuda(out, "out");
+  check_cuda(lse, "lse");
+  const int T = qkv.size(0);
+  auto dqkv = torch::empty_like(qkv);
+  auto delta = torch::empty({T, nh}, qkv.options().dtype(torch::kFloat));
+  bcfl::AttnBwdParams p{};
+  p.qkv = qkv.data_ptr();
+  p.out = out.data_ptr();
+  p.dout = dout.data_ptr();
+  p.lse = lse.data_ptr<float>();
+  p.delta = delta.data_ptr<float>();
+  p.dqkv = dqkv.data_ptr();
+  p.cu = cu.data_ptr<int>();
+  p.B = cu.numel() - 1;
+  p.T = T;
+  p.nh = nh; p.nkv = nkv; p.d = d; p.max_s = max_s;
+  p.scale = (float)scale;
+  p.causal = causal;
+  p.p8 = (uint32_t)p8; p.ka = (uint32_t)ka; p.kb = (uint32_t)kb;
+  if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_bwd(p, stream()), "attn_bwd");
+  return dqkv;
+}
+
+// ------------------------------------------------------------------------------------------------
+std::vector<Tensor> emb_ln_fwd(Tensor ids, Tensor pos, optional<Tensor> tt, Tensor word,
+                               optional<Tensor> posw, optional<Tensor> typew, Tensor gamma,
+                               Tensor beta, double eps, int64_t p8, int64_t ka, int64_t kb) {
+  check_cuda(ids, "ids");
+  check_cuda(word, "word_embeddings");
+  TORCH_CHECK(ids.scalar_type() == at::kInt && pos.scalar_type() == at::kInt, "ids must be int32");
+  const int T = ids.numel(), H = word.size(1);
+  auto out = torch::empty({T, H}, word.options());
+  auto z = torch::empty({T, H}, word.options());
+  auto f = word.options().dtype(torch::kFloat);
+  auto mean = torch::empty({T}, f), rstd = torch::empty({T}, f);
+  const int* ttp = tt.has_value() && tt->defined() ? tt->data_ptr<int>() : nullptr;
+  check_rc(bcfl::launch_emb_ln_fwd(ids.data_ptr<int>(), pos.data_ptr<int>(), ttp, word.data_ptr(),
+                                   ptr_or_null(posw), ptr_or_null(typew), gamma.data_ptr(),
+                                   beta.data_ptr(), out.data_ptr(), z.data_ptr(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), T, H, (float)eps,
+                                   (uint32_t)p8, (uint32_t)ka, (uint32_t)kb, dt_of(word), stream()),
+           "emb_ln_fwd");
+  return {out, z, mean, rstd};
+}
+
+std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Tensor> tt, Tensor z,
+                               Tensor mean, Tensor rstd, Tensor gamma, int64_t V, int64_t P,
+                               int64_t TV, int64_t p8, int64_t ka, int64_t kb) {
+  check_cuda(dout, "dout");
+  const int T = ids.numel(), H = z.size(1);
+  auto f = z.options().dtype(torch::kFloat);
+  auto dword = torch::zeros({V, H}, f);
+  Tensor dpos = P > 0 ? torch::zeros({P, H}, f) : Tensor();
+  Tensor dtype_ = TV > 0 ? torch::zeros({TV, H}, f) : Tensor();
+  const int nblk = bcfl::bwd_blocks(T);
+  auto partial = torch::empty({nblk, 3, H}, f);
+  const int* ttp = tt.has_value() && tt->defined() ? tt->data_ptr<int>() : nullptr;
+  const int dt = dt_of(z);
+  check_rc(bcfl::launch_emb_ln_bwd(dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(),
+                                   rstd.data_ptr<float>(), gamma.data_ptr(), ids.data_ptr<int>(),
+                                   pos.data_ptr<int>(), ttp, dword.data_ptr<float>(),
+                                   P > 0 ? dpos.data_ptr<float>() : nullptr,
+                                   TV > 0 ? dtype_.data_ptr<float>() : nullptr,
+                                   partial.data_ptr<float>(), nblk, T, H, (uint32_t)p8,
+                                   (uint32_t)ka, (uint32_t)kb, dt, stream()),
+           "emb_ln_bwd");
+  auto popt = z.options();
+  auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);
+  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 0, H, dgamma.data_ptr(), dt, stream()), "colsum");
+  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 1, H, dbeta.data_ptr(), dt, stream()), "colsum");
+  if (TV > 0 && ttp == nullptr) {  // implicit type id 0: row 0 gets the column sum of dz
+    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 2, H, dtype_.data_ptr(),
+                                 bcfl::DT_F32, stream()), "colsum");
+  }
+  return {dword, dpos, dtype_, dgamma, dbeta};
+}
+
+std::vector<Tensor> rmsnorm_fwd(Tensor x, Tensor w, double eps) {
+  check_cuda(x, "x");
+  const int H = x.size(-1);
+  const int T = x.numel() / H;
+  auto out = torch::empty_like(x);
+  auto rstd = torch::empty({T}, x.options().dtype(torch::kFloat));
+  check_rc(bcfl::launch_rmsnorm_fwd(x.data_ptr(), w.data_ptr(), out.data_ptr(),
+                                    rstd.data_ptr<float>(), T, H, (float)eps, dt_of(x), stream()),
+           "rmsnorm_fwd");
+  return {out, rstd};
+}
+
+std::vector<Tensor> rmsnorm_bwd(Tensor dout, Tensor x, Tensor w, Tensor rstd, bool need_dw) {
+  check_cuda(dout, "dout");
+  const int H = x.size(-1);
+  const int T = x.numel() / H;
+  auto dx = torch::empty_like(x);
+  const int nblk = bcfl::bwd_blocks(T);
+  Tensor partial;
+  if (need_dw) partial = torch::empty({nblk, H}, x.options().dtype(torch::kFloat));
+  check_rc(bcfl::launch_rmsnorm_bwd(dout.data_ptr(), x.data_ptr(), w.data_ptr(),
+                                    rstd.data_ptr<float>(), dx.data_ptr(),
+                                    need_dw ? partial.data_ptr<float>() : nullptr, nblk, T, H,
+                                    dt_of(x), stream()),
+           "rmsnorm_bwd");
+  Tensor dw;
+  if (need_dw) {
+    dw = torch::empty({H}, w.options());
+    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 1, 0, H, dw.data_ptr(), dt_of(w), stream()), "colsum");
+  }
+  return {dx, dw};
+}
+
+Tensor rope_fwd(Tensor x, Tensor pos, Tensor cos, Tensor sin, int64_t nrot, int64_t d, bool inverse) {
+  check_cuda(x, "x");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat, "rope tables must be fp32");
+  auto out = torch::empty_like(x);
+  const int stride = x.size(-1);
+  check_rc(bcfl::launch_rope(x.data_ptr(), out.data_ptr(), pos.data_ptr<int>(),
+                             cos.data_ptr<float>(), sin.data_ptr<float>(), x.numel() / stride,
+                             stride, nrot, d, inverse ? 1 : 0, dt_of(x), stream()),
+           "rope");
+  return out;
+}
+
+Tensor swiglu_fwd(Tensor gu) {
+  check_cuda(gu, "gate_up");
+  const int I = gu.size(-1) / 2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  auto out = torch::empty(sizes, gu.options());
+  check_rc(bcfl::launch_swiglu_fwd(gu.data_ptr(), out.data_ptr(), gu.numel() / (2 * I), I,
+                                   dt_of(gu), stream()), "swiglu_fwd");
+  return out;
+}
+
+Tensor swiglu_bwd(Tensor dout, Tensor gu) {
+  check_cuda(dout, "dout");
+  const int I = gu.size(-1) / 2;
+  auto dgu = torch::empty_like(gu);
+  check_rc(bcfl::launch_swiglu_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(),
+                                   gu.numel() / (2 * I), I, dt_of(gu), stream()), "swiglu_bwd");
+  return dgu;
+}
+
+// ------------------------------------------------------------------------------------------------
+void adamw(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> param_out, double lr,
+           double b1, double b2, double eps, double wd, int64_t step, int64_t mode,
+           double grad_scale) {
+  check_cuda(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
+              v.scalar_type() == at::kFloat, "AdamW state must be fp32");
+  TORCH_CHECK(grad.numel() == master.numel() && m.numel() == master.numel(), "AdamW sizes");
+  const bool po = param_out.has_value() && param_out->defined();
+  check_rc(bcfl::launch_adamw(master.data_ptr<float>(), grad.data_ptr(), dt_of(grad),
+                              m.data_ptr<float>(), v.data_ptr<float>(),
+                              po ? param_out->data_ptr() : nullptr, po ? dt_of(*param_out) : -1,
+                              (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
+                              (int)mode, (float)grad_scale, master.numel(), stream()),
+           "adamw");
+}
+
+void mix(Tensor master, std::vector<Tensor> nbrs, double self_w, std::vector<double> w,
+         optional<Tensor> param_out) {
+  check_cuda(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat, "master must be fp32");
+  TORCH_CHECK(nbrs.size() == w.size(), "weights/neighbours");
+  std::vector<const void*> ptrs;
+  std::vector<int> dts;
+  std::vector<float> ws;
+  for (size_t i = 0; i < nbrs.size(); ++i) {
+    check_cuda(nbrs[i], "neighbour");
+    TORCH_CHECK(nbrs[i].numel() == master.numel(), "neighbour size");
+    ptrs.push_back(nbrs[i].data_ptr());
+    dts.push_back(dt_of(nbrs[i]));
+    ws.push_back((float)w[i]);
+  }
+  const bool po = param_out.has_value() && param_out->defined();
+  check_rc(bcfl::launch_mix(master.data_ptr<float>(), ptrs.data(), dts.data(), ws.data(),
+                            (int)ptrs.size(), (float)self_w, po ? param_out->data_ptr() : nullptr,
+                            po ? dt_of(*param_out) : -1, master.numel(), stream()),
+           "mix");
+}
+
+void axpby(Tensor y, Tensor x, double a, double b) {
+  check_cuda(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kFloat, "axpby target must be fp32");
+  check_rc(bcfl::launch_axpby(y.data_ptr<float>(), x.data_ptr(), dt_of(x), (float)a, (float)b,
+                              y.numel(), stream()), "axpby");
+}
+
+void cast_copy(Tensor dst, Tensor src) {
+  check_cuda(dst, "dst");
+  check_cuda(src, "src");
+  TORCH_CHECK(dst.numel() == src.numel(), "cast_copy size");
+  check_rc(bcfl::launch_cast_copy(dst.data_ptr(), dt_of(dst), src.data_ptr(), dt_of(src),
+                                  dst.numel(), stream()), "cast_copy");
+}
+
+void delta_encode(Tensor x, Tensor ref, Tensor out) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && ref.scalar_type() == at::kFloat, "fp32 state");
+  check_rc(bcfl::launch_delta_encode(x.data_ptr<float>(), ref.data_ptr<float>(), out.data_ptr(),
+                                     dt_of(out), x.numel(), stream()), "delta_encode");
+}
+
+Tensor block_sketch(Tensor x, int64_t dim, int64_t ka, int64_t kb) {
+  check_cuda(x, "x");
+  auto out = torch::empty({dim}, x.options().dtype(torch::kFloat));
+  check_rc(bcfl::launch_block_sketch(x.data_ptr(), dt_of(x), x.numel(), (int)dim, (uint32_t)ka,
+                                     (uint32_t)kb, out.data_ptr<float>(), stream()),
+           "block_sketch");
+  return out;
+}
+
+Tensor sha256_leaves(Tensor buf, int64_t leaf_bytes) {
+  check_cuda(buf, "buf");
+  const int64_t nbytes = buf.numel() * buf.element_size();
+  const int64_t n = std::max<int64_t>(1, (nbytes + leaf_bytes - 1) / leaf_bytes);
+  auto out = torch::empty({n, 32}, buf.options().dtype(torch::kUInt8));
+  check_rc(bcfl::launch_sha256_leaves(static_cast<const uint8_t*>(buf.data_ptr()), nbytes,
+                                      leaf_bytes, out.data_ptr<uint8_t>(), n, stream()),
+           "sha256_leaves");
+  return out;
+}
+
+Tensor sha256_merkle(Tensor leaves) {
+  check_cuda(leaves, "leaves");
+  auto work = leaves.clone();
+  auto scratch = torch::empty_like(leaves);
+  auto root = torch::empty({32}, leaves.options());
+  check_rc(bcfl::launch_sha256_merkle(work.data_ptr<uint8_t>(), scratch.data_ptr<uint8_t>(),
+                                      leaves.size(0), root.data_ptr<uint8_t>(), stream()),
+           "sha256_merkle");
+  return root;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "bcfl gfx950 (CDNA4) kernels";
+  m.def("bdaln_fwd", &bdaln_fwd);
+  m.def("bdaln_bwd", &bdaln_bwd);
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("emb_ln_fwd", &emb_ln_fwd);
+  m.def("emb_ln_bwd", &emb_ln_bwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_fwd", &rope_fwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("adamw", &adamw);
+  m.def("mix", &mix);
+  m.def("axpby", &axpby);
+  m.def("cast_copy", &cast_copy);
+  m.def("delta_encode", &delta_encode);
+  m.def("block_sketch", &block_sketch);
+  m.def("sha256_leaves", &sha256_leaves);
+  m.def("sha256_merkle", &sha256_merkle);
+}

@@ -1,0 +1,509 @@
+// K4: varlen flash attention forward + backward on MFMA (gfx950), bf16 in, fp32 accumulate.
+//
+// What it replaces: HF BERT 4.35 runs attention EAGER in the reference (matmul -> /8 -> +mask ->
+// softmax -> dropout -> matmul on [32,12,512,512] padded scores). Here rows are
+// packed (cu_seqlens), padding is never computed, the S x S matrix is never materialised, and the
+// dropout mask is regenerated from a counter hash in the backward pass.
+//
+// Geometry (all kernels): workgroup = 4 waves (256 threads); each wave owns 32 rows of the
+// "outer" dimension and the workgroup shares 64-row tiles of the "inner" dimension through LDS.
+//   fwd  : wave = 32 queries; K/V tiles of 64 keys staged in LDS.
+//   dq   : wave = 32 queries; recompute S, P and dP against K/V tiles; dQ += dS K.
+//   dkdv : wave = 32 keys (K, V fragments stay in registers); Q/dO tiles of 64 queries staged in
+//          LDS; dV += P^T dO, dK += dS^T Q accumulate in registers over every query (and every
+//          query head of the GQA group) — no atomics, deterministic.
+//
+// MFMA mapping (v_mfma_f32_32x32x16_bf16, see cdna_hip_programming.md §3): the score tile is
+// computed SWAPPED in fwd/dq (S^T = K Q^T: the query is the accumulator COLUMN = lane, so the
+// softmax row statistics are lane-local plus one xor-32 shuffle), and the accumulator feeds the
+// next MFMA directly as its B operand ("accumulator as operand", k-order 16s+8(j>>2)+4h+(j&3)).
+// The A operand of that second product needs the other tensor column-wise: it is read with
+// ds_read_b64_tr_b16 (hardware transpose) from a row-major LDS tile.
+// LDS row strides: K/Q/dO tiles HD*2+16 B (conflict-free 16-lane ds_read_b128 row reads);
+// V tiles HD*2+64 B (conflict-free 32-lane transposed reads).
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace bcfl {
+namespace {
+
+constexpr int NWAVE = 4;
+constexpr int ROWS = 32;              // rows per wave
+constexpr int BLK = NWAVE * ROWS;     // 128 outer rows per workgroup
+constexpr int TILE = 64;              // inner tile
+constexpr int DROP_STRIDE = 8192;     // dropout element index = (tq*nh + h)*8192 + key_pos
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+
+__device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8_t lds_row8(const bf16_t* p) {
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
+
+__device__ __forceinline__ s16x4_t tr4(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
+}
+
+// A operand holding X[k][r] for k = kb + {0..3} (elements 0..3) and kb + 8 + {0..3} (4..7), where
+// X is a row-major LDS tile [k][col] with row stride `stride`, lane column r = col0 + (lane & 31).
+// Per 16-lane group g: block rows kb..kb+3, columns col0 + 16(g&1) .. +15.
+__device__ __forceinline__ bf16x8_t tr_operand(const bf16_t* tile, int stride, int kb, int col0,
+                                               int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
+  const bf16_t* p0 = tile + (kb + q) * stride + col0 + 16 * (g & 1) + 4 * pc;
+  const s16x4_t lo = tr4(p0);
+  const s16x4_t hi = tr4(p0 + 8 * stride);
+  const s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__device__ __forceinline__ f32x16_t zero16() {
+  f32x16_t z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// row offset inside a 32x32 accumulator: reg -> row (reg&3) + 8(reg>>2) + 4h
+__device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
+
+// ------------------------------------------------------------------------------------------------
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+  constexpr int KS = HD + 8;   // K row stride (elements)
+  constexpr int VS = HD + 32;  // V row stride
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Vs = Ks + TILE * KS;
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tok0 = p.cu[b];
+  const int L = p.cu[b + 1] - tok0;
+  const int q0 = blockIdx.x * BLK;
+  if (q0 >= L) return;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int qw0 = q0 + wid * ROWS;
+  const bool active = qw0 < L;
+  const int hk = h / (p.nh / p.nkv);
+  const int rs = (p.nh + 2 * p.nkv) * HD;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  const int koff = p.nh * HD + hk * HD;
+  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+
+  bf16x8_t qf[HD / 16];
+  {
+    const int qi = min(qw0 + r, L - 1);
+    const bf16_t* qrow = qkv + (size_t)(tok0 + qi) * rs + h * HD;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qrow + 16 * s + 8 * hh);
+  }
+  f32x16_t o[HD / 32];
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u) o[u] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = p.scale * LOG2E;
+  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const int myq = qw0 + r;
+  const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
+  const int kend = p.causal ? min(L, q0 + BLK) : L;
+
+  for (int k0 = 0; k0 < kend; k0 += TILE) {
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
+      const int kr = idx / (HD / 8), c = idx % (HD / 8);
+      const int key = k0 + kr;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (key < L) {
+        const bf16_t* base = qkv + (size_t)(tok0 + key) * rs;
+        kv = *reinterpret_cast<const uint4*>(base + koff + c * 8);
+        vv = *reinterpret_cast<const uint4*>(base + voff + c * 8);
+      }
+      *reinterpret_cast<uint4*>(Ks + kr * KS + c * 8) = kv;
+      *reinterpret_cast<uint4*>(Vs + kr * VS + c * 8) = vv;
+    }
+    __syncthreads();
+    if (!active) continue;
+    if (p.causal && k0 > qw0 + ROWS - 1) continue;
+
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sacc[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s)
+        sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int key = k0 + 32 * t + acc_row(reg, hh);
+        float v = sacc[t][reg] * sl2;
+        if (key >= L || (p.causal && key > myq)) v = -INFINITY;
+        sacc[t][reg] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) o[u][reg] *= alpha;
+    m = mn;
+
+    bf16x8_t pf[4];
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        uint32_t hsh = 0;
+        if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int reg = 4 * g4 + e;
+          float pv = exp2f(sacc[t][reg] - mn);
+          ls += pv;
+          if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv * sd : 0.f;
+          pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
+        }
+      }
+    l += ls;
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8_t a = tr_operand(Vs, VS, 16 * ks + 4 * hh, 32 * u, lane);
+        o[u] = mfma32(a, pf[ks], o[u]);
+      }
+  }
+  if (!active) return;
+  l += __shfl_xor(l, 32, 64);
+  if (myq >= L) return;
+  const float inv = 1.f / l;
+  bf16_t* orow = reinterpret_cast<bf16_t*>(p.out) + (size_t)(tok0 + myq) * p.nh * HD + h * HD;
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float v[4] = {o[u][4 * g4] * inv, o[u][4 * g4 + 1] * inv, o[u][4 * g4 + 2] * inv,
+                          o[u][4 * g4 + 3] * inv};
+      Vec4<bf16_t>::store(orow + 32 * u + 8 * g4 + 4 * hh, v);
+    }
+  if (hh == 0) p.lse[(size_t)(tok0 + myq) * p.nh + h] = (m + log2f(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------------------------
+// delta[t, h] = sum_d dO * O
+template <int HD>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ dout,
+                                                        const bf16_t* __restrict__ out,
+                                                        float* __restrict__ delta, int64_t rows) {
+  constexpr int LPR = HD / 8;  // lanes per (t, h) row
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t row = gid / LPR;
+  const int c = gid % LPR;
+  float a = 0.f;
+  if (row < rows) {
+    const uint4 x = *reinterpret_cast<const uint4*>(dout + row * HD + c * 8);
+    const uint4 y = *reinterpret_cast<const uint4*>(out + row * HD + c * 8);
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      a += __uint_as_float(xs[k] << 16) * __uint_as_float(ys[k] << 16) +
+           __uint_as_float(xs[k] & 0xffff0000u) * __uint_as_float(ys[k] & 0xffff0000u);
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (row < rows && c == 0) delta[row] = a;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
+  constexpr int KS = HD + 8;  // K: row reads (S^T) + transposed reads (dQ)
+  constexpr int VS = HD + 8;  // V: row reads (dP^T)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Vs = Ks + TILE * KS;
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tok0 = p.cu[b];
+  const int L = p.cu[b + 1] - tok0;
+  const int q0 = blockIdx.x * BLK;
+  if (q0 >= L) return;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int qw0 = q0 + wid * ROWS;
+  const bool active = qw0 < L;
+  const int hk = h / (p.nh / p.nkv);
+  const int rs = (p.nh + 2 * p.nkv) * HD;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
+  const int koff = p.nh * HD + hk * HD;
+  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+  const int myq = qw0 + r;
+  const int qi = min(myq, L - 1);
+
+  bf16x8_t qf[HD / 16], df[HD / 16];
+  {
+    const bf16_t* qrow = qkv + (size_t)(tok0 + qi) * rs + h * HD;
+    const bf16_t* drow_ = dout + (size_t)(tok0 + qi) * p.nh * HD + h * HD;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8_t*>(qrow + 16 * s + 8 * hh);
+      df[s] = *reinterpret_cast<const bf16x8_t*>(drow_ + 16 * s + 8 * hh);
+    }
+  }
+  const float lse2 = p.lse[(size_t)(tok0 + qi) * p.nh + h] * LOG2E;
+  const float dlt = p.delta[(size_t)(tok0 + qi) * p.nh + h];
+  f32x16_t dq[HD / 32];
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u) dq[u] = zero16();
+  const float sl2 = p.scale * LOG2E;
+  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
+  const int kend = p.causal ? min(L, q0 + BLK) : L;
+
+  for (int k0 = 0; k0 < kend; k0 += TILE) {
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
+      const int kr = idx / (HD / 8), c = idx % (HD / 8);
+      const int key = k0 + kr;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (key < L) {
+        const bf16_t* base = qkv + (size_t)(tok0 + key) * rs;
+        kv = *reinterpret_cast<const uint4*>(base + koff + c * 8);
+        vv = *reinterpret_cast<const uint4*>(base + voff + c * 8);
+      }
+      *reinterpret_cast<uint4*>(Ks + kr * KS + c * 8) = kv;
+      *reinterpret_cast<uint4*>(Vs + kr * VS + c * 8) = vv;
+    }
+    __syncthreads();
+    if (!active) continue;
+    if (p.causal && k0 > qw0 + ROWS - 1) continue;
+
+    f32x16_t sacc[2], pacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sacc[t] = zero16();
+      pacc[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s) {
+        sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
+        pacc[t] = mfma32(lds_row8(Vs + (32 * t + r) * VS + 16 * s + 8 * hh), df[s], pacc[t]);
+      }
+    }
+    bf16x8_t dsf[4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        uint32_t hsh = 0;
+        if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int reg = 4 * g4 + e;
+          const int key = k0 + 32 * t + acc_row(reg, hh);
+          float pv = exp2f(sacc[t][reg] * sl2 - lse2);
+          if (key >= L || (p.causal && key > myq)) pv = 0.f;
+          float dp = pacc[t][reg];
+          if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp * sd : 0.f;
+          dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        dq[u] = mfma32(tr_operand(Ks, KS, 16 * ks + 4 * hh, 32 * u, lane), dsf[ks], dq[u]);
+  }
+  if (!active || myq >= L) return;
+  bf16_t* dst = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + myq) * rs + h * HD;
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float v[4] = {dq[u][4 * g4] * p.scale, dq[u][4 * g4 + 1] * p.scale,
+                          dq[u][4 * g4 + 2] * p.scale, dq[u][4 * g4 + 3] * p.scale};
+      Vec4<bf16_t>::store(dst + 32 * u + 8 * g4 + 4 * hh, v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
+  constexpr int QS = HD + 8;  // Q / dO tiles: row reads + transposed reads
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Ds = Qs + TILE * QS;
+  float* lse_s = reinterpret_cast<float*>(Ds + TILE * QS);
+  float* dl_s = lse_s + TILE;
+
+  const int b = blockIdx.z, hk = blockIdx.y;
+  const int tok0 = p.cu[b];
+  const int L = p.cu[b + 1] - tok0;
+  const int kb0 = blockIdx.x * BLK;
+  if (kb0 >= L) return;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int kw0 = kb0 + wid * ROWS;
+  const bool active = kw0 < L;
+  const int rs = (p.nh + 2 * p.nkv) * HD;
+  const int grp = p.nh / p.nkv;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
+  const int koff = p.nh * HD + hk * HD;
+  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+  const int mykey = kw0 + r;
+  const int ki = min(mykey, L - 1);
+
+  bf16x8_t kf[HD / 16], vf[HD / 16];
+  {
+    const bf16_t* base = qkv + (size_t)(tok0 + ki) * rs;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8_t*>(base + koff + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const bf16x8_t*>(base + voff + 16 * s + 8 * hh);
+    }
+  }
+  f32x16_t dk[HD / 32], dv[HD / 32];
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv[u] = zero16(); }
+  const float sl2 = p.scale * LOG2E;
+  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const int qstart = p.causal ? (kb0 / TILE) * TILE : 0;
+
+  for (int hq = hk * grp; hq < (hk + 1) * grp; ++hq) {
+    for (int q0 = qstart; q0 < L; q0 += TILE) {
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
+        const int qr = idx / (HD / 8), c = idx % (HD / 8);
+        const int q = q0 + qr;
+        uint4 qv = make_uint4(0, 0, 0, 0), dv_ = make_uint4(0, 0, 0, 0);
+        if (q < L) {
+          qv = *reinterpret_cast<const uint4*>(qkv + (size_t)(tok0 + q) * rs + hq * HD + c * 8);
+          dv_ = *reinterpret_cast<const uint4*>(dout + (size_t)(tok0 + q) * p.nh * HD + hq * HD + c * 8);
+        }
+        *reinterpret_cast<uint4*>(Qs + qr * QS + c * 8) = qv;
+        *reinterpret_cast<uint4*>(Ds + qr * QS + c * 8) = dv_;
+      }
+      if (threadIdx.x < TILE) {
+        const int q = q0 + threadIdx.x;
+        lse_s[threadIdx.x] = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E : 0.f;
+        dl_s[threadIdx.x] = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] : 0.f;
+      }
+      __syncthreads();
+      if (!active) continue;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int qt0 = q0 + 32 * t;
+        if (p.causal && qt0 + 31 < kw0) continue;  // every query of the subtile precedes my keys
+        f32x16_t sacc = zero16(), pacc = zero16();
+#pragma unroll
+        for (int s = 0; s < HD / 16; ++s) {
+          sacc = mfma32(lds_row8(Qs + (32 * t + r) * QS + 16 * s + 8 * hh), kf[s], sacc);
+          pacc = mfma32(lds_row8(Ds + (32 * t + r) * QS + 16 * s + 8 * hh), vf[s], pacc);
+        }
+        bf16x8_t pf[2], dsf[2];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int ql = 32 * t + 8 * g4 + 4 * hh;  // 4 consecutive queries
+          const float4 ls4 = *reinterpret_cast<const float4*>(lse_s + ql);
+          const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + ql);
+          const float lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int reg = 4 * g4 + e;
+            const int q = q0 + ql + e;
+            float pv = exp2f(sacc[reg] * sl2 - lsv[e]);
+            if (q >= L || (p.causal && mykey > q)) pv = 0.f;
+            float pd = pv, dp = pacc[reg];
+            if (p.p8) {
+              const uint32_t idx = (uint32_t)((tok0 + q) * p.nh + hq) * (uint32_t)DROP_STRIDE + (uint32_t)mykey;
+              const bool keep = keep_elem(idx, p.p8, p.ka, p.kb);
+              pd = keep ? pv * sd : 0.f;
+              dp = keep ? dp * sd : 0.f;
+            }
+            pf[reg >> 3][reg & 7] = (__bf16)pd;
+            dsf[reg >> 3][reg & 7] = (__bf16)(pv * (dp - dlv[e]));
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            dv[u] = mfma32(tr_operand(Ds, QS, 32 * t + 16 * s2 + 4 * hh, 32 * u, lane), pf[s2], dv[u]);
+            dk[u] = mfma32(tr_operand(Qs, QS, 32 * t + 16 * s2 + 4 * hh, 32 * u, lane), dsf[s2], dk[u]);
+          }
+      }
+    }
+  }
+  if (!active || mykey >= L) return;
+  bf16_t* drow = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + mykey) * rs;
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float kv[4] = {dk[u][4 * g4] * p.scale, dk[u][4 * g4 + 1] * p.scale,
+                           dk[u][4 * g4 + 2] * p.scale, dk[u][4 * g4 + 3] * p.scale};
+      const float vv[4] = {dv[u][4 * g4], dv[u][4 * g4 + 1], dv[u][4 * g4 + 2], dv[u][4 * g4 + 3]};
+      Vec4<bf16_t>::store(drow + koff + 32 * u + 8 * g4 + 4 * hh, kv);
+      Vec4<bf16_t>::store(drow + voff + 32 * u + 8 * g4 + 4 * hh, vv);
+    }
+}
+
+}  // namespace
+
+template <int HD>
+void fwd_hd(const AttnParams& p, hipStream_t s) {
+  dim3 grid((p.max_s + BLK - 1) / BLK, p.nh, p.B);
+  const size_t lds = (size_t)TILE * ((HD + 8) + (HD + 32)) * 2;
+  hipLaunchKernelGGL(attn_fwd_kernel<HD>, grid, dim3(256), lds, s, p);
+}
+
+template <int HD>
+void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
+  const int64_t rows = (int64_t)p.T * p.nh;
+  dim3 gq((p.max_s + BLK - 1) / BLK, p.nh, p.B);
+  dim3 gk((p.max_s + BLK - 1) / BLK, p.nkv, p.B);
+  const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
+  const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
+  hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
+                     dim3(256), 0, s, dout, out, p.delta, rows);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)TILE * 2 * (HD + 8) * 2, s, p);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, gk, dim3(256),
+                     (size_t)TILE * 2 * (HD + 8) * 2 + 2 * TILE * 4, s, p);
+}
+
+int launch_attn_fwd(const AttnParams& p, hipStream_t s) {
+  if (p.nh % p.nkv) return -2;
+  switch (p.d) {
+    case 32: fwd_hd<32>(p, s); break;
+    case 64: fwd_hd<64>(p, s); break;
+    case 128: fwd_hd<128>(p, s); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+int launch_attn_bwd(const AttnBwdParams& p, hipStream_t s) {
+  if (p.nh % p.nkv) return -2;
+  switch (p.d) {
+    case 32: bwd_hd<32>(p, s); break;
+    case 64: bwd_hd<64>(p, s); break;
+    case 128: bwd_hd<128>(p, s); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+}  // namespace bcfl

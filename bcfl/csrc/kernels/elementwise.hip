@@ -1,0 +1,482 @@
+// Memory-bound fused kernels (SURVEY.md §2.6 K6, K10, K11 + Llama SwiGLU/RoPE).
+//
+//   bias_act_fwd/bwd   GEMM epilogue: bias + GELU(erf) / gelu_new(tanh) / ReLU / tanh / SiLU, and
+//                      its backward with the bias-gradient column sum fused in (K6)
+//   swiglu_fwd/bwd     silu(gate) * up on the fused [T, 2I] gate|up projection
+//   rope               rotate the q|k column blocks of a packed qkv projection (HF rotate_half)
+//   adamw              ONE launch over the whole flat parameter buffer (K10), HF or torch semantics
+//   mix / axpby / delta_encode / cast_copy   FedAvg scale-accumulate + gossip mixing (K11) and the
+//                      error-feedback bf16 delta codec of the P2P wire
+//   block_sketch       signed block sketch of a flat update for the anomaly filter
+//
+// All kernels use 4-wide vector accesses (8 B bf16 / 16 B fp32 per lane) and grid-stride loops
+// sized to the CU count (Guideline 11: ≤ 8 blocks per CU resident, rest grid-strided).
+#include "common.h"
+#include "kernels.h"
+
+namespace bcfl {
+namespace {
+
+constexpr int EW_THREADS = 256;
+
+inline int ew_grid(int64_t nvec) {
+  int64_t g = (nvec + EW_THREADS - 1) / EW_THREADS;
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+enum Act { ACT_GELU = 0, ACT_GELU_TANH = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4 };
+
+__device__ __forceinline__ float act_f(float x, int act) {
+  switch (act) {
+    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_GELU_TANH: {
+      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_TANH: return tanhf(x);
+    default: return x / (1.f + __expf(-x));
+  }
+}
+
+__device__ __forceinline__ float act_d(float x, int act) {
+  switch (act) {
+    case ACT_GELU:
+      return 0.5f * (1.f + erff(x * 0.70710678118654752f)) +
+             x * 0.3989422804014327f * __expf(-0.5f * x * x);
+    case ACT_GELU_TANH: {
+      const float k = 0.7978845608028654f;
+      const float u = k * (x + 0.044715f * x * x * x);
+      const float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+    }
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_TANH: { const float t = tanhf(x); return 1.f - t * t; }
+    default: { const float sg = 1.f / (1.f + __expf(-x)); return sg * (1.f + x * (1.f - sg)); }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void bias_act_fwd_kernel(const T* __restrict__ y,
+                                                                  const T* __restrict__ bias,
+                                                                  T* __restrict__ out,
+                                                                  int64_t nvec, int N, int act) {
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    const int64_t e = i * 4;
+    const int col = (int)(e % N);
+    float v[4], b[4] = {0.f, 0.f, 0.f, 0.f};
+    Vec4<T>::load(y + e, v);
+    if (bias) Vec4<T>::load(bias + col, b);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = act_f(v[k] + b[k], act);
+    Vec4<T>::store(out + e, v);
+  }
+}
+
+// grid (ceil(N / (4*256)), nblk_rows); partial[blockIdx.y][N]
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void bias_act_bwd_kernel(
+    const T* __restrict__ dout, const T* __restrict__ y, const T* __restrict__ bias,
+    T* __restrict__ dy, float* __restrict__ partial, int64_t rows, int N, int act) {
+  const int col = (blockIdx.x * EW_THREADS + threadIdx.x) * 4;
+  if (col >= N) return;
+  float b[4] = {0.f, 0.f, 0.f, 0.f}, acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) Vec4<T>::load(bias + col, b);
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const int64_t e = r * N + col;
+    float d[4], v[4], o[4];
+    Vec4<T>::load(dout + e, d);
+    Vec4<T>::load(y + e, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = d[k] * act_d(v[k] + b[k], act);
+      acc[k] += o[k];
+    }
+    Vec4<T>::store(dy + e, o);
+  }
+  if (partial) {
+    float4 a = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(partial + (size_t)blockIdx.y * N + col) = a;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void swiglu_fwd_kernel(const T* __restrict__ gu,
+                                                                T* __restrict__ out, int64_t nvec,
+                                                                int I) {
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    const int64_t e = i * 4;
+    const int64_t r = e / I;
+    const int c = (int)(e % I);
+    float g[4], u[4], o[4];
+    Vec4<T>::load(gu + r * 2 * I + c, g);
+    Vec4<T>::load(gu + r * 2 * I + I + c, u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = g[k] / (1.f + __expf(-g[k])) * u[k];
+    Vec4<T>::store(out + e, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void swiglu_bwd_kernel(const T* __restrict__ dout,
+                                                                const T* __restrict__ gu,
+                                                                T* __restrict__ dgu,
+                                                                int64_t nvec, int I) {
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    const int64_t e = i * 4;
+    const int64_t r = e / I;
+    const int c = (int)(e % I);
+    float d[4], g[4], u[4], dg[4], du[4];
+    Vec4<T>::load(dout + e, d);
+    Vec4<T>::load(gu + r * 2 * I + c, g);
+    Vec4<T>::load(gu + r * 2 * I + I + c, u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float sg = 1.f / (1.f + __expf(-g[k]));
+      const float sl = g[k] * sg;
+      du[k] = d[k] * sl;
+      dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
+    }
+    Vec4<T>::store(dgu + r * 2 * I + c, dg);
+    Vec4<T>::store(dgu + r * 2 * I + I + c, du);
+  }
+}
+
+// one thread per (row, rotated pair) or per copied element pair
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void rope_kernel(const T* __restrict__ x, T* __restrict__ out,
+                                                         const int* __restrict__ pos,
+                                                         const float* __restrict__ cosb,
+                                                         const float* __restrict__ sinb,
+                                                         int64_t rows, int stride, int nrot, int d,
+                                                         int inverse) {
+  const int half = d / 2;
+  const int per_row = stride / 2;  // work items per row
+  const int64_t total = rows * per_row;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    const int64_t r = i / per_row;
+    const int w = (int)(i % per_row);
+    const int64_t rb = r * stride;
+    const int rot_items = nrot * half;
+    if (w < rot_items) {
+      const int h = w / half, j = w % half;
+      const int p = pos[r];
+      const float c = cosb[(int64_t)p * half + j];
+      const float s = inverse ? -sinb[(int64_t)p * half + j] : sinb[(int64_t)p * half + j];
+      const int64_t a = rb + (int64_t)h * d + j;
+      const float x1 = ld<T>(x, a), x2 = ld<T>(x, a + half);
+      st<T>(out, a, x1 * c - x2 * s);
+      st<T>(out, a + half, x2 * c + x1 * s);
+    } else {
+      const int64_t a = rb + (int64_t)nrot * d + 2 * (w - rot_items);
+      st<T>(out, a, ld<T>(x, a));
+      st<T>(out, a + 1, ld<T>(x, a + 1));
+    }
+  }
+}
+
+template <typename TD, typename TS>
+__global__ __launch_bounds__(EW_THREADS) void cast_kernel(TD* __restrict__ dst,
+                                                         const TS* __restrict__ src, int64_t n) {
+  const int64_t nvec = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float v[4];
+    Vec4<TS>::load(src + i * 4, v);
+    Vec4<TD>::store(dst + i * 4, v);
+  }
+  for (int64_t i = nvec * 4 + blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * EW_THREADS)
+    st<TD>(dst, i, ld<TS>(src, i));
+}
+
+template <typename TX>
+__global__ __launch_bounds__(EW_THREADS) void axpby_kernel(float* __restrict__ y, const TX* x,
+                                                          float a, float b, int64_t n) {
+  const int64_t nvec = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float yv[4], xv[4];
+    Vec4<float>::load(y + i * 4, yv);
+    if (a != 0.f) Vec4<TX>::load(x + i * 4, xv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) yv[k] = (a != 0.f ? a * xv[k] : 0.f) + b * yv[k];
+    Vec4<float>::store(y + i * 4, yv);
+  }
+  for (int64_t i = nvec * 4 + blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * EW_THREADS)
+    y[i] = (a != 0.f ? a * ld<TX>(x, i) : 0.f) + b * y[i];
+}
+
+constexpr int MAX_NBRS = 16;
+struct MixArgs {
+  const void* p[MAX_NBRS];
+  int dt[MAX_NBRS];
+  float w[MAX_NBRS];
+};
+
+__global__ __launch_bounds__(EW_THREADS) void mix_kernel(float* __restrict__ master, MixArgs args,
+                                                        int nn, float self_w,
+                                                        bf16_t* __restrict__ pout_bf,
+                                                        float* __restrict__ pout_f, int64_t n) {
+  const int64_t nvec = n / 4;  // n is a multiple of 64 (flat buffers are padded)
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float acc[4];
+    Vec4<float>::load(master + i * 4, acc);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] *= self_w;
+    for (int j = 0; j < nn; ++j) {
+      float v[4];
+      if (args.dt[j] == DT_BF16) Vec4<bf16_t>::load((const bf16_t*)args.p[j] + i * 4, v);
+      else Vec4<float>::load((const float*)args.p[j] + i * 4, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += args.w[j] * v[k];
+    }
+    Vec4<float>::store(master + i * 4, acc);
+    if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, acc);
+    if (pout_f) Vec4<float>::store(pout_f + i * 4, acc);
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(EW_THREADS) void delta_encode_kernel(const float* __restrict__ x,
+                                                                 float* __restrict__ ref,
+                                                                 TO* __restrict__ out, int64_t n) {
+  const int64_t nvec = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float xv[4], rv[4], q[4];
+    Vec4<float>::load(x + i * 4, xv);
+    Vec4<float>::load(ref + i * 4, rv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = xv[k] - rv[k];
+      q[k] = sizeof(TO) == 2 ? bf2f(f2bf(d)) : d;
+      rv[k] += q[k];
+    }
+    Vec4<TO>::store(out + i * 4, q);
+    Vec4<float>::store(ref + i * 4, rv);
+  }
+}
+
+template <typename TG>
+__global__ __launch_bounds__(EW_THREADS) void adamw_kernel(
+    float* __restrict__ master, const TG* __restrict__ grad, float* __restrict__ m,
+    float* __restrict__ v, bf16_t* __restrict__ pout_bf, float* __restrict__ pout_f, float b1,
+    float b2, float eps, float step_size, float decay_mul, float denom_scale, int hf_mode,
+    float grad_scale, int64_t n) {
+  const int64_t nvec = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float p[4], g[4], mm[4], vv[4];
+    Vec4<float>::load(master + i * 4, p);
+    Vec4<TG>::load(grad + i * 4, g);
+    Vec4<float>::load(m + i * 4, mm);
+    Vec4<float>::load(v + i * 4, vv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = g[k] * grad_scale;
+      mm[k] = b1 * mm[k] + (1.f - b1) * gk;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
+      if (hf_mode) {
+        p[k] -= step_size * mm[k] / (sqrtf(vv[k]) + eps);
+        p[k] *= decay_mul;
+      } else {
+        p[k] *= decay_mul;
+        p[k] -= step_size * mm[k] / (sqrtf(vv[k]) * denom_scale + eps);
+      }
+    }
+    Vec4<float>::store(master + i * 4, p);
+    Vec4<float>::store(m + i * 4, mm);
+    Vec4<float>::store(v + i * 4, vv);
+    if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, p);
+    if (pout_f) Vec4<float>::store(pout_f + i * 4, p);
+  }
+}
+
+template <typename TX>
+__global__ __launch_bounds__(EW_THREADS) void block_sketch_kernel(const TX* __restrict__ x,
+                                                                 int64_t n, int64_t blk,
+                                                                 uint32_t ka, uint32_t kb,
+                                                                 float* __restrict__ out) {
+  __shared__ float red[EW_THREADS / WAVE];
+  const int64_t lo = (int64_t)blockIdx.x * blk;
+  const int64_t hi = lo + blk < n ? lo + blk : n;
+  float a = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += EW_THREADS) {
+    const uint32_t h = hash32((uint32_t)i, ka, kb);
+    const float s = (h & 1u) ? 1.f : -1.f;
+    a += s * ld<TX>(x, i);
+  }
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < EW_THREADS / WAVE; ++w) t += red[w];
+    out[blockIdx.x] = t;
+  }
+}
+
+}  // namespace
+
+int launch_bias_act_fwd(const void* y, const void* bias, void* out, int64_t rows, int N, int act,
+                        int dt, hipStream_t s) {
+  if (N % 4) return -2;
+  const int64_t nvec = rows * N / 4;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(bias_act_fwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)y, (const bf16_t*)bias, (bf16_t*)out, nvec, N, act);
+  else
+    hipLaunchKernelGGL(bias_act_fwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const float*)y, (const float*)bias, (float*)out, nvec, N, act);
+  return 0;
+}
+
+int launch_bias_act_bwd(const void* dout, const void* y, const void* bias, void* dy,
+                        float* partial, int nblk_rows, int64_t rows, int N, int act, int dt,
+                        hipStream_t s) {
+  if (N % 4) return -2;
+  dim3 grid((N / 4 + EW_THREADS - 1) / EW_THREADS, nblk_rows);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(bias_act_bwd_kernel<bf16_t>, grid, dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)bias, (bf16_t*)dy,
+                       partial, rows, N, act);
+  else
+    hipLaunchKernelGGL(bias_act_bwd_kernel<float>, grid, dim3(EW_THREADS), 0, s,
+                       (const float*)dout, (const float*)y, (const float*)bias, (float*)dy,
+                       partial, rows, N, act);
+  return 0;
+}
+
+int launch_swiglu_fwd(const void* gu, void* out, int64_t rows, int I, int dt, hipStream_t s) {
+  if (I % 4) return -2;
+  const int64_t nvec = rows * I / 4;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(swiglu_fwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)gu, (bf16_t*)out, nvec, I);
+  else
+    hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const float*)gu, (float*)out, nvec, I);
+  return 0;
+}
+
+int launch_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, int I, int dt,
+                      hipStream_t s) {
+  if (I % 4) return -2;
+  const int64_t nvec = rows * I / 4;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(swiglu_bwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, nvec, I);
+  else
+    hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
+                       (const float*)dout, (const float*)gu, (float*)dgu, nvec, I);
+  return 0;
+}
+
+int launch_rope(const void* x, void* out, const int* pos, const float* cos, const float* sin,
+                int64_t rows, int row_stride, int nrot, int d, int inverse, int dt, hipStream_t s) {
+  if (row_stride % 2 || d % 2 || nrot * d > row_stride) return -2;
+  const int64_t total = rows * (row_stride / 2);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(rope_kernel<bf16_t>, dim3(ew_grid(total)), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)x, (bf16_t*)out, pos, cos, sin, rows, row_stride, nrot, d, inverse);
+  else
+    hipLaunchKernelGGL(rope_kernel<float>, dim3(ew_grid(total)), dim3(EW_THREADS), 0, s,
+                       (const float*)x, (float*)out, pos, cos, sin, rows, row_stride, nrot, d, inverse);
+  return 0;
+}
+
+int launch_cast_copy(void* dst, int dst_dt, const void* src, int src_dt, int64_t n, hipStream_t s) {
+  const int g = ew_grid(n / 4 + 1);
+  if (dst_dt == DT_BF16 && src_dt == DT_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(g), dim3(EW_THREADS), 0, s, (bf16_t*)dst, (const float*)src, n);
+  else if (dst_dt == DT_F32 && src_dt == DT_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(g), dim3(EW_THREADS), 0, s, (float*)dst, (const bf16_t*)src, n);
+  else if (dst_dt == DT_F32 && src_dt == DT_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(EW_THREADS), 0, s, (float*)dst, (const float*)src, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(g), dim3(EW_THREADS), 0, s, (bf16_t*)dst, (const bf16_t*)src, n);
+  return 0;
+}
+
+int launch_axpby(float* y, const void* x, int x_dt, float a, float b, int64_t n, hipStream_t s) {
+  const int g = ew_grid(n / 4 + 1);
+  if (x_dt == DT_BF16)
+    hipLaunchKernelGGL(axpby_kernel<bf16_t>, dim3(g), dim3(EW_THREADS), 0, s, y, (const bf16_t*)x, a, b, n);
+  else
+    hipLaunchKernelGGL(axpby_kernel<float>, dim3(g), dim3(EW_THREADS), 0, s, y, (const float*)x, a, b, n);
+  return 0;
+}
+
+int launch_mix(float* master, const void* const* nbrs, const int* nbr_dt, const float* w, int nn,
+               float self_w, void* param_out, int param_dt, int64_t n, hipStream_t s) {
+  if (n % 4) return -2;
+  if (nn > MAX_NBRS) {  // fold in chunks of MAX_NBRS
+    int r = launch_mix(master, nbrs, nbr_dt, w, MAX_NBRS, self_w, nullptr, param_dt, n, s);
+    if (r) return r;
+    return launch_mix(master, nbrs + MAX_NBRS, nbr_dt + MAX_NBRS, w + MAX_NBRS, nn - MAX_NBRS,
+                      1.f, param_out, param_dt, n, s);
+  }
+  MixArgs a;
+  for (int j = 0; j < nn; ++j) { a.p[j] = nbrs[j]; a.dt[j] = nbr_dt[j]; a.w[j] = w[j]; }
+  hipLaunchKernelGGL(mix_kernel, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, master, a, nn,
+                     self_w, param_dt == DT_BF16 ? (bf16_t*)param_out : nullptr,
+                     param_dt == DT_F32 ? (float*)param_out : nullptr, n);
+  return 0;
+}
+
+int launch_delta_encode(const float* x, float* ref, void* out, int out_dt, int64_t n, hipStream_t s) {
+  if (n % 4) return -2;
+  if (out_dt == DT_BF16)
+    hipLaunchKernelGGL(delta_encode_kernel<bf16_t>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, x, ref, (bf16_t*)out, n);
+  else
+    hipLaunchKernelGGL(delta_encode_kernel<float>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, x, ref, (float*)out, n);
+  return 0;
+}
+
+int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* v,
+                 void* param_out, int param_dt, float lr, float b1, float b2, float eps, float wd,
+                 int step, int mode, float grad_scale, int64_t n, hipStream_t s) {
+  if (n % 4) return -2;
+  const double bc1 = 1.0 - __builtin_pow((double)b1, step);
+  const double bc2 = 1.0 - __builtin_pow((double)b2, step);
+  float step_size, decay_mul, denom_scale = 1.f;
+  const int hf = mode == 0;
+  if (hf) {
+    step_size = (float)(lr * __builtin_sqrt(bc2) / bc1);
+    decay_mul = 1.f - lr * wd;
+  } else {
+    step_size = (float)(lr / bc1);
+    decay_mul = 1.f - lr * wd;
+    denom_scale = (float)(1.0 / __builtin_sqrt(bc2));
+  }
+  bf16_t* pb = param_dt == DT_BF16 ? (bf16_t*)param_out : nullptr;
+  float* pf = param_dt == DT_F32 ? (float*)param_out : nullptr;
+  if (grad_dt == DT_BF16)
+    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, master,
+                       (const bf16_t*)grad, m, v, pb, pf, b1, b2, eps, step_size, decay_mul,
+                       denom_scale, hf, grad_scale, n);
+  else
+    hipLaunchKernelGGL(adamw_kernel<float>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, master,
+                       (const float*)grad, m, v, pb, pf, b1, b2, eps, step_size, decay_mul,
+                       denom_scale, hf, grad_scale, n);
+  return 0;
+}
+
+int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
+                        float* out, hipStream_t s) {
+  const int64_t blk = (n + dim - 1) / dim;
+  if (x_dt == DT_BF16)
+    hipLaunchKernelGGL(block_sketch_kernel<bf16_t>, dim3(dim), dim3(EW_THREADS), 0, s, (const bf16_t*)x, n, blk, ka, kb, out);
+  else
+    hipLaunchKernelGGL(block_sketch_kernel<float>, dim3(dim), dim3(EW_THREADS), 0, s, (const float*)x, n, blk, ka, kb, out);
+  return 0;
+}
+
+}  // namespace bcfl

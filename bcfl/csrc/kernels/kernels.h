@@ -1,0 +1,91 @@
+// Host launchers of the bcfl gfx950 kernels (raw pointers + hipStream_t; no torch headers, so
+// the .hip translation units compile fast and bindings.cpp owns all tensor plumbing).
+// Every launcher returns 0 on success, <0 for an unsupported shape (the binding raises).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bcfl {
+
+enum DType { DT_F32 = 0, DT_BF16 = 1 };
+
+// ---- layernorm.hip ----------------------------------------------------------------------------
+int bwd_blocks(int T);
+int launch_bdaln_fwd(const void* y, const void* bias, const void* res, const void* gamma,
+                     const void* beta, void* out, void* z, float* mean, float* rstd, int T, int H,
+                     float eps, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
+int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
+                     const void* gamma, void* dz, void* dy, float* partial, int nblk, int T, int H,
+                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s);
+int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,
+                  hipStream_t s);
+int launch_emb_ln_fwd(const int* ids, const int* pos, const int* tt, const void* word,
+                      const void* posw, const void* typew, const void* gamma, const void* beta,
+                      void* out, void* z, float* mean, float* rstd, int T, int H, float eps,
+                      uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
+int launch_emb_ln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
+                      const void* gamma, const int* ids, const int* pos, const int* tt,
+                      float* dword, float* dpos, float* dtype, float* partial, int nblk, int T,
+                      int H, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
+int launch_rmsnorm_fwd(const void* x, const void* w, void* out, float* rstd, int T, int H,
+                       float eps, int dt, hipStream_t s);
+int launch_rmsnorm_bwd(const void* dout, const void* x, const void* w, const float* rstd, void* dx,
+                       float* partial, int nblk, int T, int H, int dt, hipStream_t s);
+
+// ---- elementwise.hip -----------------------------------------------------------------------------
+int launch_bias_act_fwd(const void* y, const void* bias, void* out, int64_t rows, int N, int act,
+                        int dt, hipStream_t s);
+int launch_bias_act_bwd(const void* dout, const void* y, const void* bias, void* dy,
+                        float* partial, int nblk_rows, int64_t rows, int N, int act, int dt,
+                        hipStream_t s);
+int launch_swiglu_fwd(const void* gu, void* out, int64_t rows, int I, int dt, hipStream_t s);
+int launch_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, int I, int dt,
+                      hipStream_t s);
+int launch_rope(const void* x, void* out, const int* pos, const float* cos, const float* sin,
+                int64_t rows, int row_stride, int nrot, int d, int inverse, int dt, hipStream_t s);
+int launch_cast_copy(void* dst, int dst_dt, const void* src, int src_dt, int64_t n, hipStream_t s);
+int launch_axpby(float* y, const void* x, int x_dt, float a, float b, int64_t n, hipStream_t s);
+int launch_mix(float* master, const void* const* nbrs, const int* nbr_dt, const float* w, int nn,
+               float self_w, void* param_out, int param_dt, int64_t n, hipStream_t s);
+int launch_delta_encode(const float* x, float* ref, void* out, int out_dt, int64_t n,
+                        hipStream_t s);
+int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* v,
+                 void* param_out, int param_dt, float lr, float b1, float b2, float eps, float wd,
+                 int step, int mode, float grad_scale, int64_t n, hipStream_t s);
+int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
+                        float* out, hipStream_t s);
+
+// ---- sha256.hip ------------------------------------------------------------------------------------
+int launch_sha256_leaves(const uint8_t* data, int64_t nbytes, int64_t leaf_bytes, uint8_t* out,
+                         int64_t nleaves, hipStream_t s);
+// reduces [n, 32] digests to one root in place-ish using scratch (same size); returns ptr to root
+int launch_sha256_merkle(uint8_t* level, uint8_t* scratch, int64_t n, uint8_t* root, hipStream_t s);
+
+// ---- attention.hip -----------------------------------------------------------------------------
+struct AttnParams {
+  const void* qkv;     // [T, (nh + 2 nkv) * d] bf16
+  void* out;           // [T, nh * d] bf16
+  float* lse;          // [T, nh] (natural log, of scale * q.k)
+  const int* cu;       // [B + 1]
+  int B, T, nh, nkv, d, max_s;
+  float scale;
+  int causal;
+  uint32_t p8, ka, kb;
+};
+struct AttnBwdParams {
+  const void* qkv;
+  const void* out;
+  const void* dout;    // [T, nh * d]
+  const float* lse;    // [T, nh]
+  float* delta;        // [T, nh] scratch: rowsum(dO * O)
+  void* dqkv;          // [T, (nh + 2 nkv) * d]
+  const int* cu;
+  int B, T, nh, nkv, d, max_s;
+  float scale;
+  int causal;
+  uint32_t p8, ka, kb;
+};
+int launch_attn_fwd(const AttnParams& p, hipStream_t s);
+int launch_attn_bwd(const AttnBwdParams& p, hipStream_t s);
+
+}  // namespace bcfl

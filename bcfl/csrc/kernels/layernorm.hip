@@ -1,0 +1,545 @@
+// K1/K2: fused normalisation kernels.
+//
+//   bdaln_fwd / bdaln_bwd   LN(dropout(y + bias) + residual): the BERT post-GEMM epilogue that the
+//                           reference runs as 4 separate eager ops (bias add, dropout, residual add,
+//                           LayerNorm) 25x per step (HF BertSelfOutput / BertOutput).
+//   emb_ln_fwd / emb_ln_bwd word+position+type gather, sum, LN, dropout (HF BertEmbeddings).
+//   rmsnorm_fwd / rmsnorm_bwd Llama RMSNorm.
+//
+// Layout: ONE wave64 per row; lane l owns the 4-element chunks l, l+64, ... (8-byte bf16 loads, a
+// fully coalesced 512 B per wave-instruction), fp32 statistics with two passes over registers.
+// Backward column sums (dgamma/dbeta/dbias) accumulate in registers across the rows a wave visits,
+// are combined across the 4 waves of the block in LDS, and written as one fp32 partial row-set
+// per block; colsum_kernel reduces the partials and casts to the parameter dtype.
+#include "common.h"
+#include "kernels.h"
+
+namespace bcfl {
+
+namespace {
+
+constexpr int LN_THREADS = 256;
+constexpr int LN_WAVES = LN_THREADS / WAVE;
+
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void bdaln_fwd_kernel(
+    const TA* __restrict__ y, const TP* __restrict__ bias, const TA* __restrict__ res,
+    const TP* __restrict__ gamma, const TP* __restrict__ beta, TA* __restrict__ out,
+    TA* __restrict__ zsave, float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
+    int H, float eps, uint32_t p8, uint32_t ka, uint32_t kb) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  const float sc = p8 ? keep_scale(p8) : 1.f;
+  float v[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      Vec4<TA>::load(y + base + col, v[i]);
+      if (bias) {
+        float b[4];
+        Vec4<TP>::load(bias + col, b);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += b[k];
+      }
+      if (p8) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[i][k] = keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? v[i][k] * sc : 0.f;
+      }
+      if (res) {
+        float r[4];
+        Vec4<TA>::load(res + base + col, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += r[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += v[i][k];
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { float d = v[i][k] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / H + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      if (zsave) Vec4<TA>::store(zsave + base + col, v[i]);
+      float g[4] = {1.f, 1.f, 1.f, 1.f}, bt[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
+      if (gamma) Vec4<TP>::load(gamma + col, g);
+      if (beta) Vec4<TP>::load(beta + col, bt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (v[i][k] - mean) * rstd * g[k] + bt[k];
+      Vec4<TA>::store(out + base + col, o);
+    }
+  }
+  if (lane == 0 && mean_out) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// partial[block][k][H], k = 0: dgamma, 1: dbeta, 2: dbias
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
+    const TA* __restrict__ dout, const TA* __restrict__ z, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const TP* __restrict__ gamma, TA* __restrict__ dz_out,
+    TA* __restrict__ dy_out, float* __restrict__ partial, int T, int H, uint32_t p8, uint32_t ka,
+    uint32_t kb, int want_dbias) {
+  __shared__ float red[LN_WAVES][3][NCH * 4 * WAVE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float sc = p8 ? keep_scale(p8) : 1.f;
+  float dg[NCH][4], db[NCH][4], dbi[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dg[i][k] = db[i][k] = dbi[i][k] = 0.f;
+  float gm[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      if (gamma) Vec4<TP>::load(gamma + col, gm[i]);
+      else { gm[i][0] = gm[i][1] = gm[i][2] = gm[i][3] = 1.f; }
+    }
+  }
+  for (int row = blockIdx.x * LN_WAVES + wid; row < T; row += gridDim.x * LN_WAVES) {
+    const size_t base = (size_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NCH][4], g[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+        float d[4], zz[4];
+        Vec4<TA>::load(dout + base + col, d);
+        Vec4<TA>::load(z + base + col, zz);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[i][k] = (zz[k] - mean) * rstd;
+          g[i][k] = d[k] * gm[i][k];
+          s1 += g[i][k];
+          s2 += g[i][k] * xh[i][k];
+          dg[i][k] += d[k] * xh[i][k];
+          db[i][k] += d[k];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+        float dz[4], dy[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dz[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
+          dy[k] = p8 ? (keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? dz[k] * sc : 0.f) : dz[k];
+          dbi[i][k] += dy[k];
+        }
+        Vec4<TA>::store(dz_out + base + col, dz);
+        if (dy_out) Vec4<TA>::store(dy_out + base + col, dy);
+      }
+    }
+  }
+  // combine the block's waves
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = (i * WAVE + lane) * 4 + k;
+      red[wid][0][j] = dg[i][k];
+      red[wid][1][j] = db[i][k];
+      red[wid][2][j] = dbi[i][k];
+    }
+  __syncthreads();
+  const int nk = want_dbias ? 3 : 2;
+  for (int j = threadIdx.x; j < H; j += LN_THREADS) {
+    for (int k = 0; k < nk; ++k) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < LN_WAVES; ++w) a += red[w][k][j];
+      partial[((size_t)blockIdx.x * 3 + k) * H + j] = a;
+    }
+  }
+}
+
+template <typename TP>
+__global__ void colsum_kernel(const float* __restrict__ partial, int nblk, int nk_stride, int k,
+                              int H, TP* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= H) return;
+  float a = 0.f;
+  for (int b = 0; b < nblk; ++b) a += partial[((size_t)b * nk_stride + k) * H + j];
+  st<TP>(out, j, a);
+}
+
+// ---------------------------------- embeddings + LN ------------------------------------------
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void emb_ln_fwd_kernel(
+    const int* __restrict__ ids, const int* __restrict__ pos, const int* __restrict__ tt,
+    const TP* __restrict__ word, const TP* __restrict__ posw, const TP* __restrict__ typew,
+    const TP* __restrict__ gamma, const TP* __restrict__ beta, TA* __restrict__ out,
+    TA* __restrict__ zsave, float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
+    int H, float eps, uint32_t p8, uint32_t ka, uint32_t kb) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  const size_t wb = (size_t)ids[row] * H;
+  const size_t pb = posw ? (size_t)pos[row] * H : 0;
+  const size_t tb = typew ? (size_t)(tt ? tt[row] : 0) * H : 0;
+  float v[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      Vec4<TP>::load(word + wb + col, v[i]);
+      float a[4];
+      if (posw) {
+        Vec4<TP>::load(posw + pb + col, a);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += a[k];
+      }
+      if (typew) {
+        Vec4<TP>::load(typew + tb + col, a);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += a[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += v[i][k];
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { float d = v[i][k] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / H + eps);
+  const float sc = p8 ? keep_scale(p8) : 1.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      Vec4<TA>::store(zsave + base + col, v[i]);
+      float g[4], bt[4], o[4];
+      Vec4<TP>::load(gamma + col, g);
+      Vec4<TP>::load(beta + col, bt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[k] = (v[i][k] - mean) * rstd * g[k] + bt[k];
+        if (p8) o[k] = keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? o[k] * sc : 0.f;
+      }
+      Vec4<TA>::store(out + base + col, o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// partial k: 0 dgamma, 1 dbeta, 2 dtype-row-0 (when type ids are implicit zeros)
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void emb_ln_bwd_kernel(
+    const TA* __restrict__ dout, const TA* __restrict__ z, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const TP* __restrict__ gamma, const int* __restrict__ ids,
+    const int* __restrict__ pos, const int* __restrict__ tt, float* __restrict__ dword,
+    float* __restrict__ dpos, float* __restrict__ dtype, float* __restrict__ partial, int T, int H,
+    uint32_t p8, uint32_t ka, uint32_t kb) {
+  __shared__ float red[LN_WAVES][3][NCH * 4 * WAVE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float sc = p8 ? keep_scale(p8) : 1.f;
+  const bool type_sum = dtype != nullptr && tt == nullptr;
+  float dg[NCH][4], db[NCH][4], dt[NCH][4], gm[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dg[i][k] = db[i][k] = dt[i][k] = 0.f;
+    if (col < H) Vec4<TP>::load(gamma + col, gm[i]);
+  }
+  for (int row = blockIdx.x * LN_WAVES + wid; row < T; row += gridDim.x * LN_WAVES) {
+    const size_t base = (size_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NCH][4], g[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+        float d[4], zz[4];
+        Vec4<TA>::load(dout + base + col, d);
+        Vec4<TA>::load(z + base + col, zz);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (p8) d[k] = keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? d[k] * sc : 0.f;
+          xh[i][k] = (zz[k] - mean) * rstd;
+          g[i][k] = d[k] * gm[i][k];
+          s1 += g[i][k];
+          s2 += g[i][k] * xh[i][k];
+          dg[i][k] += d[k] * xh[i][k];
+          db[i][k] += d[k];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+    const size_t wb = (size_t)ids[row] * H;
+    const size_t pb = dpos ? (size_t)pos[row] * H : 0;
+    const size_t tb = (dtype && tt) ? (size_t)tt[row] * H : 0;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float dz = rstd * (g[i][k] - s1 - xh[i][k] * s2);
+          atomicAdd(dword + wb + col + k, dz);
+          if (dpos) atomicAdd(dpos + pb + col + k, dz);
+          if (dtype && tt) atomicAdd(dtype + tb + col + k, dz);
+          if (type_sum) dt[i][k] += dz;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = (i * WAVE + lane) * 4 + k;
+      red[wid][0][j] = dg[i][k];
+      red[wid][1][j] = db[i][k];
+      red[wid][2][j] = dt[i][k];
+    }
+  __syncthreads();
+  for (int j = threadIdx.x; j < H; j += LN_THREADS) {
+    for (int k = 0; k < 3; ++k) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < LN_WAVES; ++w) a += red[w][k][j];
+      partial[((size_t)blockIdx.x * 3 + k) * H + j] = a;
+    }
+  }
+}
+
+// ----------------------------------------- RMSNorm -------------------------------------------------
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void rmsnorm_fwd_kernel(
+    const TA* __restrict__ x, const TP* __restrict__ w, TA* __restrict__ out,
+    float* __restrict__ rstd_out, int T, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  float v[NCH][4];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      Vec4<TA>::load(x + base + col, v[i]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ss += v[i][k] * v[i][k];
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / H + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+    if (col < H) {
+      float g[4], o[4];
+      Vec4<TP>::load(w + col, g);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = v[i][k] * r * g[k];
+      Vec4<TA>::store(out + base + col, o);
+    }
+  }
+  if (lane == 0) rstd_out[row] = r;
+}
+
+template <typename TA, typename TP, int NCH>
+__global__ __launch_bounds__(LN_THREADS) void rmsnorm_bwd_kernel(
+    const TA* __restrict__ dout, const TA* __restrict__ x, const TP* __restrict__ w,
+    const float* __restrict__ rstd_in, TA* __restrict__ dx, float* __restrict__ partial, int T,
+    int H) {
+  __shared__ float red[LN_WAVES][NCH * 4 * WAVE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float dw[NCH][4], gm[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = (lane + i * WAVE) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dw[i][k] = 0.f;
+    if (col < H) Vec4<TP>::load(w + col, gm[i]);
+  }
+  for (int row = blockIdx.x * LN_WAVES + wid; row < T; row += gridDim.x * LN_WAVES) {
+    const size_t base = (size_t)row * H;
+    const float r = rstd_in[row];
+    float xv[NCH][4], g[NCH][4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+        float d[4];
+        Vec4<TA>::load(dout + base + col, d);
+        Vec4<TA>::load(x + base + col, xv[i]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          g[i][k] = d[k] * gm[i][k];
+          s += g[i][k] * xv[i][k];
+          dw[i][k] += d[k] * xv[i][k] * r;
+        }
+      }
+    }
+    s = wave_sum(s) / H;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = r * g[i][k] - xv[i][k] * r * r * r * s;
+        Vec4<TA>::store(dx + base + col, o);
+      }
+    }
+  }
+  if (partial) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[wid][(i * WAVE + lane) * 4 + k] = dw[i][k];
+    __syncthreads();
+    for (int j = threadIdx.x; j < H; j += LN_THREADS) {
+      float a = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < LN_WAVES; ++w2) a += red[w2][j];
+      partial[(size_t)blockIdx.x * H + j] = a;
+    }
+  }
+}
+
+inline int nchunks(int H) { return (H / 4 + WAVE - 1) / WAVE; }
+
+#define NCH_DISPATCH(H, ...)                                                    \
+  switch (nchunks(H)) {                                                         \
+    case 1: { constexpr int NC = 1; __VA_ARGS__; break; }                       \
+    case 2: { constexpr int NC = 2; __VA_ARGS__; break; }                       \
+    case 3: { constexpr int NC = 3; __VA_ARGS__; break; }                       \
+    case 4: { constexpr int NC = 4; __VA_ARGS__; break; }                       \
+    case 5: case 6: { constexpr int NC = 6; __VA_ARGS__; break; }               \
+    case 7: case 8: { constexpr int NC = 8; __VA_ARGS__; break; }               \
+    case 9: case 10: case 11: case 12: { constexpr int NC = 12; __VA_ARGS__; break; } \
+    case 13: case 14: case 15: case 16: { constexpr int NC = 16; __VA_ARGS__; break; } \
+    default: return -1;                                                         \
+  }
+
+#define NCH_DISPATCH_SMALL(H, ...)                                              \
+  switch (nchunks(H)) {                                                         \
+    case 1: { constexpr int NC = 1; __VA_ARGS__; break; }                       \
+    case 2: { constexpr int NC = 2; __VA_ARGS__; break; }                       \
+    case 3: { constexpr int NC = 3; __VA_ARGS__; break; }                       \
+    case 4: { constexpr int NC = 4; __VA_ARGS__; break; }                       \
+    case 5: case 6: { constexpr int NC = 6; __VA_ARGS__; break; }               \
+    case 7: case 8: { constexpr int NC = 8; __VA_ARGS__; break; }               \
+    default: return -1;                                                         \
+  }
+
+#define DT_DISPATCH(dt, ...)                                                    \
+  if (dt == DT_BF16) { using TA = bf16_t; using TP = bf16_t; __VA_ARGS__; }     \
+  else { using TA = float; using TP = float; __VA_ARGS__; }
+
+}  // namespace
+
+int bwd_blocks(int T) {
+  int b = (T + LN_WAVES * 8 - 1) / (LN_WAVES * 8);
+  return b < 1 ? 1 : (b > 256 ? 256 : b);
+}
+
+int launch_bdaln_fwd(const void* y, const void* bias, const void* res, const void* gamma,
+                     const void* beta, void* out, void* z, float* mean, float* rstd, int T, int H,
+                     float eps, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  dim3 grid((T + LN_WAVES - 1) / LN_WAVES);
+  DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((bdaln_fwd_kernel<TA, TP, NC>), grid,
+      dim3(LN_THREADS), 0, s, (const TA*)y, (const TP*)bias, (const TA*)res, (const TP*)gamma,
+      (const TP*)beta, (TA*)out, (TA*)z, mean, rstd, T, H, eps, p8, ka, kb)));
+  return 0;
+}
+
+int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
+                     const void* gamma, void* dz, void* dy, float* partial, int nblk, int T, int H,
+                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((bdaln_bwd_kernel<TA, TP, NC>), dim3(nblk),
+      dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)z, mean, rstd, (const TP*)gamma,
+      (TA*)dz, (TA*)dy, partial, T, H, p8, ka, kb, want_dbias)));
+  return 0;
+}
+
+int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,
+                  hipStream_t s) {
+  dim3 grid((H + 255) / 256);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, partial, nblk, nk_stride, k, H, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, partial, nblk, nk_stride, k, H, (float*)out);
+  return 0;
+}
+
+int launch_emb_ln_fwd(const int* ids, const int* pos, const int* tt, const void* word,
+                      const void* posw, const void* typew, const void* gamma, const void* beta,
+                      void* out, void* z, float* mean, float* rstd, int T, int H, float eps,
+                      uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  dim3 grid((T + LN_WAVES - 1) / LN_WAVES);
+  DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((emb_ln_fwd_kernel<TA, TP, NC>), grid,
+      dim3(LN_THREADS), 0, s, ids, pos, tt, (const TP*)word, (const TP*)posw, (const TP*)typew,
+      (const TP*)gamma, (const TP*)beta, (TA*)out, (TA*)z, mean, rstd, T, H, eps, p8, ka, kb)));
+  return 0;
+}
+
+int launch_emb_ln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
+                      const void* gamma, const int* ids, const int* pos, const int* tt,
+                      float* dword, float* dpos, float* dtype, float* partial, int nblk, int T,
+                      int H, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((emb_ln_bwd_kernel<TA, TP, NC>), dim3(nblk),
+      dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)z, mean, rstd, (const TP*)gamma, ids,
+      pos, tt, dword, dpos, dtype, partial, T, H, p8, ka, kb)));
+  return 0;
+}
+
+int launch_rmsnorm_fwd(const void* x, const void* w, void* out, float* rstd, int T, int H,
+                       float eps, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  dim3 grid((T + LN_WAVES - 1) / LN_WAVES);
+  DT_DISPATCH(dt, NCH_DISPATCH(H, hipLaunchKernelGGL((rmsnorm_fwd_kernel<TA, TP, NC>), grid,
+      dim3(LN_THREADS), 0, s, (const TA*)x, (const TP*)w, (TA*)out, rstd, T, H, eps)));
+  return 0;
+}
+
+int launch_rmsnorm_bwd(const void* dout, const void* x, const void* w, const float* rstd, void* dx,
+                       float* partial, int nblk, int T, int H, int dt, hipStream_t s) {
+  if (H % 4) return -2;
+  DT_DISPATCH(dt, NCH_DISPATCH(H, hipLaunchKernelGGL((rmsnorm_bwd_kernel<TA, TP, NC>), dim3(nblk),
+      dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)x, (const TP*)w, rstd, (TA*)dx, partial,
+      T, H)));
+  return 0;
+}
+
+}  // namespace bcfl

@@ -16,7 +16,7 @@ import torch
 from . import ref
 from ._native import native, use_native
 
-LEAF_BYTES_DEFAULT = 1 << 16  # 64 KiB Merkle leaves
+LEAF_BYTES_DEFAULT = 1 << 12  # 4 KiB Merkle leaves (~100k leaves for BERT-base: fills the GPU)
 
 
 def adamw_(master, grad, m, v, step: int, lr: float, beta1: float, beta2: float, eps: float,
@@ -71,7 +71,9 @@ def cast_copy_(dst: torch.Tensor, src: torch.Tensor):
 
 def block_sketch(x: torch.Tensor, dim: int, seed: int = 0x5EED) -> torch.Tensor:
     if use_native(x):
-        return native().block_sketch(x, int(dim), int(seed))
+        from .rng import derive_keys
+        ka, kb = derive_keys(seed, 0)
+        return native().block_sketch(x.contiguous(), int(dim), int(ka), int(kb))
     return ref.block_sketch(x, dim, seed)
 
 

@@ -1,0 +1,266 @@
+"""GPU numerics: every HIP kernel vs the PyTorch fp32 reference of the same op (bcfl.ops.ref).
+
+Run on the MI355X box: ``python -m pytest tests -m gpu``. These tests REQUIRE the native
+extension (no eager fallback on the GPU path)."""
+import hashlib
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from bcfl import ops
+from bcfl.ops import ref, rng
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert ops.native_available(), ops.load_error()
+    assert "bcfl/_C" in ops.native().__file__.replace("\\", "/")
+
+
+def _close(a, b, atol, rtol=2e-2):
+    torch.testing.assert_close(a.float(), b.float(), atol=atol, rtol=rtol)
+
+
+def _grads_close(ga, gb, tol=3e-2):
+    # relative Frobenius error: robust for bf16 gradients of mixed scale
+    for x, y in zip(ga, gb):
+        if x is None and y is None:
+            continue
+        x, y = x.float(), y.float()
+        err = (x - y).norm() / (y.norm() + 1e-6)
+        assert err < tol, f"relative grad error {err:.4f}"
+
+
+@pytest.mark.parametrize("H", [64, 128, 768, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_bdaln_fwd_bwd(H, p, with_res):
+    torch.manual_seed(0)
+    T = 333
+    y = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = (0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    be = (0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    rng.manual_seed(7)
+    out = ops.bias_dropout_add_layernorm(y, b, r, g, be, 1e-12, p, True)
+    rng.manual_seed(7)
+    p8, ka, kb = (rng.quantize_p(p), *rng.global_rng().next()) if p > 0 else (0, 0, 0)
+    leaves = [t.detach().float().requires_grad_(True) for t in (y, b, g, be)]
+    rf = r.detach().float().requires_grad_(True) if with_res else None
+    ref_out = ref.bias_dropout_add_layernorm(leaves[0], leaves[1], rf, leaves[2], leaves[3], 1e-12, p8, ka, kb)
+    _close(out, ref_out, 3e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    ref_out.backward(go.float())
+    ours = [y.grad, b.grad, g.grad, be.grad] + ([r.grad] if with_res else [])
+    theirs = [l.grad for l in leaves] + ([rf.grad] if with_res else [])
+    _grads_close(ours, theirs)
+
+
+@pytest.mark.parametrize("act", ["gelu", "gelu_new", "relu", "tanh", "silu"])
+def test_bias_act(act):
+    torch.manual_seed(0)
+    y = torch.randn(257, 3072, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = (0.2 * torch.randn(3072, device=DEV)).bfloat16().requires_grad_(True)
+    out = ops.bias_act(y, b, act)
+    yf, bf = y.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    r = ref.bias_act(yf, bf, act)
+    _close(out, r, 2e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    r.backward(go.float())
+    _grads_close([y.grad, b.grad], [yf.grad, bf.grad])
+
+
+def _attn_case(lens, nh, nkv, d, causal, p):
+    torch.manual_seed(1)
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    T = int(cu[-1])
+    qkv = (0.5 * torch.randn(T, (nh + 2 * nkv) * d, device=DEV)).bfloat16().requires_grad_(True)
+    cu_d = torch.from_numpy(cu).to(DEV)
+    rng.manual_seed(3)
+    out = ops.varlen_attention(qkv, cu_d, cu, max(lens), nh, nkv, d, p, True, causal)
+    rng.manual_seed(3)
+    p8, ka, kb = (rng.quantize_p(p), *rng.global_rng().next()) if p > 0 else (0, 0, 0)
+    qf = qkv.detach().float().requires_grad_(True)
+    r = ref.varlen_attention(qf, nh, nkv, d, cu, 1 / math.sqrt(d), causal, p8, ka, kb)
+    _close(out, r, 2e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    r.backward(go.float())
+    _grads_close([qkv.grad], [qf.grad], 3e-2)
+
+
+@pytest.mark.parametrize("lens", [[1, 5, 64, 65, 127, 128, 129], [512, 300, 200], [33]])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_bert(lens, p):
+    _attn_case(lens, 12, 12, 64, False, p)
+
+
+@pytest.mark.parametrize("lens", [[1, 70, 200], [256]])
+def test_attention_gqa_causal_d128(lens):
+    _attn_case(lens, 8, 2, 128, True, 0.0)
+
+
+def test_attention_lse():
+    torch.manual_seed(2)
+    lens = [100, 37]
+    cu = np.array([0, 100, 137], dtype=np.int32)
+    qkv = torch.randn(137, 3 * 4 * 64, device=DEV).bfloat16()
+    out, lse = ops.native().attn_fwd(qkv, torch.from_numpy(cu).to(DEV), 100, 4, 4, 64, 0.125, False, 0, 0, 0)
+    _, rl = ref.varlen_attention(qkv.float(), 4, 4, 64, cu, 0.125, return_lse=True)
+    _close(lse, rl, 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embedding_layernorm(p):
+    torch.manual_seed(0)
+    V, P, H, T = 1000, 128, 768, 300
+    ids = torch.randint(0, V, (T,), device=DEV, dtype=torch.int32)
+    pos = torch.randint(0, P, (T,), device=DEV, dtype=torch.int32)
+    ws = [(0.02 * torch.randn(*s, device=DEV)).bfloat16().requires_grad_(True) for s in ((V, H), (P, H), (2, H))]
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    be = (0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    rng.manual_seed(11)
+    out = ops.embedding_layernorm(ids, pos, None, *ws, g, be, 1e-12, p, True)
+    rng.manual_seed(11)
+    p8, ka, kb = (rng.quantize_p(p), *rng.global_rng().next()) if p > 0 else (0, 0, 0)
+    leaves = [t.detach().float().requires_grad_(True) for t in (*ws, g, be)]
+    r = ref.embedding_layernorm(ids, pos, None, *leaves[:3], leaves[3], leaves[4], 1e-12, p8, ka, kb)
+    _close(out, r, 3e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    r.backward(go.float())
+    _grads_close([w.grad for w in ws] + [g.grad, be.grad], [l.grad for l in leaves])
+
+
+def test_rmsnorm_rope_swiglu():
+    torch.manual_seed(0)
+    T, H = 129, 512
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    out = ops.rmsnorm(x, w, 1e-5)
+    xf, wf = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    r = ref.rmsnorm(xf, wf, 1e-5)
+    _close(out, r, 3e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    r.backward(go.float())
+    _grads_close([x.grad, w.grad], [xf.grad, wf.grad])
+    # RoPE on a packed [T, (nh + 2 nkv) d] projection
+    nh, nkv, d = 4, 2, 64
+    qkv = torch.randn(T, (nh + 2 * nkv) * d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    pos = torch.arange(T, device=DEV, dtype=torch.int32) % 100
+    cos, sin = ref.rope_cache(256, d, 10000.0, DEV)
+    o = ops.rope(qkv, pos, cos, sin, nh, nkv, d)
+    qf = qkv.detach().float().requires_grad_(True)
+    nrot = nh + nkv
+    rq = torch.cat([ref.rope(qf[:, :nrot * d].reshape(T, nrot, d), pos, cos, sin).reshape(T, -1),
+                    qf[:, nrot * d:]], 1)
+    _close(o, rq, 3e-2)
+    go = torch.randn_like(o)
+    o.backward(go)
+    rq.backward(go.float())
+    _grads_close([qkv.grad], [qf.grad])
+    # SwiGLU
+    gu = torch.randn(T, 2 * 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    s = ops.swiglu(gu)
+    gf = gu.detach().float().requires_grad_(True)
+    rs_ = ref.swiglu(gf)
+    _close(s, rs_, 3e-2)
+    go = torch.randn_like(s)
+    s.backward(go)
+    rs_.backward(go.float())
+    _grads_close([gu.grad], [gf.grad])
+
+
+@pytest.mark.parametrize("mode", ["hf", "torch"])
+def test_fused_adamw(mode):
+    torch.manual_seed(0)
+    n = 1 << 20
+    master = torch.randn(n, device=DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    p_out = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    rm, rmm, rvv = master.clone(), m.clone(), v.clone()
+    for t in range(1, 4):
+        g = torch.randn(n, device=DEV).bfloat16()
+        ops.adamw_(master, g, m, v, t, 1e-3, 0.9, 0.999, 1e-6, 0.01, mode, p_out)
+        ref.adamw_(rm, g.float(), rmm, rvv, t, 1e-3, 0.9, 0.999, 1e-6, 0.01, mode)
+    _close(master, rm, 1e-5, 1e-5)
+    _close(p_out, rm, 1e-2)
+
+
+def test_flat_ops():
+    torch.manual_seed(0)
+    n = (1 << 18) + 64
+    x = torch.randn(n, device=DEV)
+    nb = [torch.randn(n, device=DEV), torch.randn(n, device=DEV).bfloat16()]
+    y = x.clone()
+    po = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ops.gossip_mix_(y, nb, 0.5, [0.3, 0.2], po)
+    _close(y, 0.5 * x + 0.3 * nb[0] + 0.2 * nb[1].float(), 1e-5, 1e-5)
+    _close(po, y, 1e-2)
+    z = x.clone()
+    ops.axpby_(z, nb[1], 2.0, -1.0)
+    _close(z, 2 * nb[1].float() - x, 1e-5, 1e-5)
+    c = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ops.cast_copy_(c, x)
+    assert torch.equal(c, x.bfloat16())
+    refb = torch.zeros(n, device=DEV)
+    q = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ops.native().delta_encode(x, refb, q)
+    assert torch.equal(q, x.bfloat16()) and torch.equal(refb, x.bfloat16().float())
+    sk = ops.block_sketch(x, 4096)
+    _close(sk, ref.block_sketch(x.cpu(), 4096).to(DEV), 1e-3, 1e-4)
+
+
+@pytest.mark.parametrize("nbytes", [4 * 1000, 4096 * 37 + 1024, 1 << 22])
+def test_sha256_merkle_matches_hashlib(nbytes):
+    g = torch.Generator().manual_seed(0)
+    host = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, generator=g)
+    dev = host.to(DEV)
+    leaf = 4096
+    b = host.numpy().tobytes()
+    leaves = [hashlib.sha256(b"\x00" + b[i:i + leaf]).digest() for i in range(0, len(b), leaf)]
+    d = ops.leaf_digests_sha256(dev, leaf).cpu()
+    assert [bytes(d[i].numpy()) for i in range(d.shape[0])] == leaves
+    from bcfl.ops.flat import merkle_from_leaves
+    assert ops.merkle_root_sha256(dev, leaf) == merkle_from_leaves(leaves)
+
+
+def test_bert_model_gpu_matches_cpu_reference():
+    from bcfl.data.batching import make_packed_batch
+    from bcfl.data.registry import load_split
+    from bcfl.models import build_model
+    m_cpu = build_model("tiny-bert", 2, seed=0).eval()
+    m_gpu = build_model("tiny-bert", 2, seed=0, device=DEV, dtype=torch.bfloat16).eval()
+    ds = load_split("tiny", "train", 2048, 128)
+    b = make_packed_batch(ds, np.arange(0, 200, 7))
+    with torch.no_grad():
+        lc = m_cpu(b)
+        lg = m_gpu(b.to(DEV)).float().cpu()
+    _close(lg, lc, 5e-2, 5e-2)
+
+
+def test_federation_gpu_smoke(tmp_path):
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=2,
+                   num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                   out_dir=str(tmp_path), reference_prints=False, anomaly_filter="both")
+    fed = Federation(cfg, verbose=False)
+    h = fed.run()
+    assert len(h) == 2 and all(np.isfinite(r["train_loss"]) for r in h)
+    assert fed.ledger.verify() == -1
+    D.set_runtime_for_tests(None)
