@@ -85,13 +85,11 @@ std::vector<Tensor> bdaln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd,
            "bdaln_bwd");
   auto popt = z.options();
   auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);
-  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 0, H, dgamma.data_ptr(), dt, stream()), "colsum");
-  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 1, H, dbeta.data_ptr(), dt, stream()), "colsum");
   Tensor dbias;
-  if (has_bias) {
-    dbias = torch::empty({H}, popt);
-    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 2, H, dbias.data_ptr(), dt, stream()), "colsum");
-  }
+  if (has_bias) dbias = torch::empty({H}, popt);
+  check_rc(bcfl::launch_colsum3(partial.data_ptr<float>(), nblk, H, dgamma.data_ptr(),
+                                dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, dt, dt,
+                                dt, stream()), "colsum3");
   return {dy, dbias, dz, dgamma, dbeta};
 }
 
@@ -112,7 +110,8 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, Tensor y, optional<Tensor> bias, i
   const int64_t rows = y.numel() / N;
   auto dy = torch::empty_like(y);
   const bool hb = bias.has_value() && bias->defined();
-  int nblk = (int)std::min<int64_t>(std::max<int64_t>(rows / 32, 1), 256);
+  // ~8 rows per thread: enough independent row-streams to hide HBM latency
+  int nblk = (int)std::min<int64_t>(std::max<int64_t>(rows / 8, 1), 1024);
   Tensor partial;
   if (hb) partial = torch::empty({nblk, N}, y.options().dtype(torch::kFloat));
   check_rc(bcfl::launch_bias_act_bwd(dout.data_ptr(), y.data_ptr(), ptr_or_null(bias),
@@ -229,12 +228,11 @@ std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Ten
            "emb_ln_bwd");
   auto popt = z.options();
   auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);
-  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 0, H, dgamma.data_ptr(), dt, stream()), "colsum");
-  check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 1, H, dbeta.data_ptr(), dt, stream()), "colsum");
-  if (TV > 0 && ttp == nullptr) {  // implicit type id 0: row 0 gets the column sum of dz
-    check_rc(bcfl::launch_colsum(partial.data_ptr<float>(), nblk, 3, 2, H, dtype_.data_ptr(),
-                                 bcfl::DT_F32, stream()), "colsum");
-  }
+  // plane 2: implicit type id 0 -> row 0 of the type table gets the column sum of dz
+  const bool tsum = TV > 0 && ttp == nullptr;
+  check_rc(bcfl::launch_colsum3(partial.data_ptr<float>(), nblk, H, dgamma.data_ptr(),
+                                dbeta.data_ptr(), tsum ? dtype_.data_ptr() : nullptr, dt, dt,
+                                bcfl::DT_F32, stream()), "colsum3");
   return {dword, dpos, dtype_, dgamma, dbeta};
 }
 
@@ -318,6 +316,36 @@ void adamw(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> para
                               (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
                               (int)mode, (float)grad_scale, master.numel(), stream()),
            "adamw");
+}
+
+void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
+              std::vector<Tensor> grads, std::vector<int64_t> offs, double lr, double b1, double b2,
+              double eps, double wd, int64_t step, int64_t mode, double grad_scale) {
+  check_cuda(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
+              v.scalar_type() == at::kFloat, "AdamW state must be fp32");
+  TORCH_CHECK(grads.size() == offs.size(), "grads / offsets");
+  if (grads.empty()) return;
+  std::vector<Tensor> keep;
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> numels;
+  const int gdt = dt_of(grads[0]);
+  for (size_t i = 0; i < grads.size(); ++i) {
+    Tensor g = grads[i].is_contiguous() ? grads[i] : grads[i].contiguous();
+    TORCH_CHECK(g.is_cuda() && dt_of(g) == gdt, "gradients must share one dtype on the GPU");
+    TORCH_CHECK(offs[i] >= 0 && offs[i] + g.numel() <= master.numel(), "gradient offset");
+    keep.push_back(g);
+    ptrs.push_back(g.data_ptr());
+    numels.push_back(g.numel());
+  }
+  const bool po = param_out.has_value() && param_out->defined();
+  check_rc(bcfl::launch_adamw_mt(master.data_ptr<float>(), m.data_ptr<float>(),
+                                 v.data_ptr<float>(), po ? param_out->data_ptr() : nullptr,
+                                 po ? dt_of(*param_out) : -1, ptrs.data(), offs.data(),
+                                 numels.data(), (int)ptrs.size(), gdt, (float)lr, (float)b1,
+                                 (float)b2, (float)eps, (float)wd, (int)step, (int)mode,
+                                 (float)grad_scale, stream()),
+           "adamw_mt");
 }
 
 void mix(Tensor master, std::vector<Tensor> nbrs, double self_w, std::vector<double> w,
@@ -413,6 +441,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("adamw", &adamw);
+  m.def("adamw_mt", &adamw_mt);
   m.def("mix", &mix);
   m.def("axpby", &axpby);
   m.def("cast_copy", &cast_copy);

@@ -61,6 +61,41 @@ template <> struct Vec4<bf16_t> {
   }
 };
 
+// 8-wide vector load/store (16 B for bf16 — the 1 KiB-per-wave-instruction sweet spot)
+template <typename T> struct Vec8;
+template <> struct Vec8<float> {
+  __device__ __forceinline__ static void load(const float* p, float v[8]) {
+    Vec4<float>::load(p, v);
+    Vec4<float>::load(p + 4, v + 4);
+  }
+  __device__ __forceinline__ static void store(float* p, const float v[8]) {
+    Vec4<float>::store(p, v);
+    Vec4<float>::store(p + 4, v + 4);
+  }
+};
+template <> struct Vec8<bf16_t> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float v[8]) {
+    uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float v[8]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]),
+                                              pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
+};
+
+// sum over the 32 lanes of a half-wave (lanes l and l^k for k < 32 share a half)
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -56,92 +56,92 @@ __device__ __forceinline__ float act_d(float x, int act) {
   }
 }
 
+// 2-D launch for row-structured elementwise kernels: grid.x covers the columns in 8-element
+// chunks (one 16-byte access per lane), grid.y strides over rows — no per-element 64-bit
+// division (which the compiler would expand into a software divide).
+constexpr int COLS_PER_BLOCK = EW_THREADS * 8;
+
 template <typename T>
 __global__ __launch_bounds__(EW_THREADS) void bias_act_fwd_kernel(const T* __restrict__ y,
                                                                   const T* __restrict__ bias,
                                                                   T* __restrict__ out,
-                                                                  int64_t nvec, int N, int act) {
-  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * EW_THREADS) {
-    const int64_t e = i * 4;
-    const int col = (int)(e % N);
-    float v[4], b[4] = {0.f, 0.f, 0.f, 0.f};
-    Vec4<T>::load(y + e, v);
-    if (bias) Vec4<T>::load(bias + col, b);
+                                                                  int64_t rows, int N, int act) {
+  const int col = (blockIdx.x * EW_THREADS + threadIdx.x) * 8;
+  if (col >= N) return;
+  float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) Vec8<T>::load(bias + col, b);
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const int64_t e = r * N + col;
+    float v[8];
+    Vec8<T>::load(y + e, v);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = act_f(v[k] + b[k], act);
-    Vec4<T>::store(out + e, v);
+    for (int k = 0; k < 8; ++k) v[k] = act_f(v[k] + b[k], act);
+    Vec8<T>::store(out + e, v);
   }
 }
 
-// grid (ceil(N / (4*256)), nblk_rows); partial[blockIdx.y][N]
+// grid (ceil(N / 2048), nblk_rows); partial[blockIdx.y][N]
 template <typename T>
 __global__ __launch_bounds__(EW_THREADS) void bias_act_bwd_kernel(
     const T* __restrict__ dout, const T* __restrict__ y, const T* __restrict__ bias,
     T* __restrict__ dy, float* __restrict__ partial, int64_t rows, int N, int act) {
-  const int col = (blockIdx.x * EW_THREADS + threadIdx.x) * 4;
+  const int col = (blockIdx.x * EW_THREADS + threadIdx.x) * 8;
   if (col >= N) return;
-  float b[4] = {0.f, 0.f, 0.f, 0.f}, acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (bias) Vec4<T>::load(bias + col, b);
+  float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) Vec8<T>::load(bias + col, b);
   for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
     const int64_t e = r * N + col;
-    float d[4], v[4], o[4];
-    Vec4<T>::load(dout + e, d);
-    Vec4<T>::load(y + e, v);
+    float d[8], v[8], o[8];
+    Vec8<T>::load(dout + e, d);
+    Vec8<T>::load(y + e, v);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       o[k] = d[k] * act_d(v[k] + b[k], act);
       acc[k] += o[k];
     }
-    Vec4<T>::store(dy + e, o);
+    Vec8<T>::store(dy + e, o);
   }
-  if (partial) {
-    float4 a = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    *reinterpret_cast<float4*>(partial + (size_t)blockIdx.y * N + col) = a;
-  }
+  if (partial) Vec8<float>::store(partial + (size_t)blockIdx.y * N + col, acc);
 }
 
 template <typename T>
 __global__ __launch_bounds__(EW_THREADS) void swiglu_fwd_kernel(const T* __restrict__ gu,
-                                                                T* __restrict__ out, int64_t nvec,
+                                                                T* __restrict__ out, int64_t rows,
                                                                 int I) {
-  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * EW_THREADS) {
-    const int64_t e = i * 4;
-    const int64_t r = e / I;
-    const int c = (int)(e % I);
-    float g[4], u[4], o[4];
-    Vec4<T>::load(gu + r * 2 * I + c, g);
-    Vec4<T>::load(gu + r * 2 * I + I + c, u);
+  const int c = (blockIdx.x * EW_THREADS + threadIdx.x) * 8;
+  if (c >= I) return;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    float g[8], u[8], o[8];
+    Vec8<T>::load(gu + r * 2 * I + c, g);
+    Vec8<T>::load(gu + r * 2 * I + I + c, u);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = g[k] / (1.f + __expf(-g[k])) * u[k];
-    Vec4<T>::store(out + e, o);
+    for (int k = 0; k < 8; ++k) o[k] = g[k] / (1.f + __expf(-g[k])) * u[k];
+    Vec8<T>::store(out + r * I + c, o);
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(EW_THREADS) void swiglu_bwd_kernel(const T* __restrict__ dout,
                                                                 const T* __restrict__ gu,
-                                                                T* __restrict__ dgu,
-                                                                int64_t nvec, int I) {
-  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * EW_THREADS) {
-    const int64_t e = i * 4;
-    const int64_t r = e / I;
-    const int c = (int)(e % I);
-    float d[4], g[4], u[4], dg[4], du[4];
-    Vec4<T>::load(dout + e, d);
-    Vec4<T>::load(gu + r * 2 * I + c, g);
-    Vec4<T>::load(gu + r * 2 * I + I + c, u);
+                                                                T* __restrict__ dgu, int64_t rows,
+                                                                int I) {
+  const int c = (blockIdx.x * EW_THREADS + threadIdx.x) * 8;
+  if (c >= I) return;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    float d[8], g[8], u[8], dg[8], du[8];
+    Vec8<T>::load(dout + r * I + c, d);
+    Vec8<T>::load(gu + r * 2 * I + c, g);
+    Vec8<T>::load(gu + r * 2 * I + I + c, u);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const float sg = 1.f / (1.f + __expf(-g[k]));
       const float sl = g[k] * sg;
       du[k] = d[k] * sl;
       dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
     }
-    Vec4<T>::store(dgu + r * 2 * I + c, dg);
-    Vec4<T>::store(dgu + r * 2 * I + I + c, du);
+    Vec8<T>::store(dgu + r * 2 * I + c, dg);
+    Vec8<T>::store(dgu + r * 2 * I + I + c, du);
   }
 }
 
@@ -299,6 +299,81 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_kernel(
   }
 }
 
+// Multi-tensor AdamW: gradients are separate tensors (as autograd produced them); master / m / v /
+// param are flat. The launch covers up to MT_MAX tensors concatenated (each padded to a multiple
+// of 4 elements); block b owns a fixed range of that concatenation and walks the tensor table.
+constexpr int MT_MAX = 40;
+struct MTArgs {
+  const void* g[MT_MAX];
+  int64_t off[MT_MAX];
+  int64_t numel[MT_MAX];
+  int64_t start[MT_MAX + 1];
+  int aligned[MT_MAX];
+  int n;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& mm, float& vv, float b1,
+                                          float b2, float eps, float step_size, float decay_mul,
+                                          float denom_scale, int hf) {
+  mm = b1 * mm + (1.f - b1) * g;
+  vv = b2 * vv + (1.f - b2) * g * g;
+  if (hf) {
+    p -= step_size * mm / (sqrtf(vv) + eps);
+    p *= decay_mul;
+  } else {
+    p *= decay_mul;
+    p -= step_size * mm / (sqrtf(vv) * denom_scale + eps);
+  }
+}
+
+template <typename TG>
+__global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
+    float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
+    bf16_t* __restrict__ pout_bf, float* __restrict__ pout_f, MTArgs a, int64_t chunk, float b1,
+    float b2, float eps, float step_size, float decay_mul, float denom_scale, int hf,
+    float grad_scale) {
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  int64_t hi = lo + chunk;
+  if (hi > a.start[a.n]) hi = a.start[a.n];
+  int t = 0;
+  while (t + 1 < a.n && a.start[t + 1] <= lo) ++t;
+  for (int64_t e = lo + threadIdx.x * 4; e < hi; e += EW_THREADS * 4) {
+    while (e >= a.start[t + 1]) ++t;
+    const int64_t loc = e - a.start[t];
+    const int64_t n = a.numel[t];
+    if (loc >= n) continue;
+    const TG* g = reinterpret_cast<const TG*>(a.g[t]) + loc;
+    const int64_t f = a.off[t] + loc;
+    if (loc + 4 <= n && a.aligned[t]) {
+      float p[4], gv[4], mm[4], vv[4];
+      Vec4<float>::load(master + f, p);
+      Vec4<TG>::load(g, gv);
+      Vec4<float>::load(m + f, mm);
+      Vec4<float>::load(v + f, vv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        adam_elem(p[k], gv[k] * grad_scale, mm[k], vv[k], b1, b2, eps, step_size, decay_mul,
+                  denom_scale, hf);
+      Vec4<float>::store(master + f, p);
+      Vec4<float>::store(m + f, mm);
+      Vec4<float>::store(v + f, vv);
+      if (pout_bf) Vec4<bf16_t>::store(pout_bf + f, p);
+      if (pout_f) Vec4<float>::store(pout_f + f, p);
+    } else {
+      for (int k = 0; k < 4 && loc + k < n; ++k) {
+        float p = master[f + k], mm = m[f + k], vv = v[f + k];
+        adam_elem(p, ld<TG>(g, k) * grad_scale, mm, vv, b1, b2, eps, step_size, decay_mul,
+                  denom_scale, hf);
+        master[f + k] = p;
+        m[f + k] = mm;
+        v[f + k] = vv;
+        if (pout_bf) pout_bf[f + k] = f2bf(p);
+        if (pout_f) pout_f[f + k] = p;
+      }
+    }
+  }
+}
+
 template <typename TX>
 __global__ __launch_bounds__(EW_THREADS) void block_sketch_kernel(const TX* __restrict__ x,
                                                                  int64_t n, int64_t blk,
@@ -327,22 +402,23 @@ __global__ __launch_bounds__(EW_THREADS) void block_sketch_kernel(const TX* __re
 
 int launch_bias_act_fwd(const void* y, const void* bias, void* out, int64_t rows, int N, int act,
                         int dt, hipStream_t s) {
-  if (N % 4) return -2;
-  const int64_t nvec = rows * N / 4;
+  if (N % 8) return -2;
+  dim3 grid((N + COLS_PER_BLOCK - 1) / COLS_PER_BLOCK, (unsigned)(rows < 8192 ? rows : 8192));
+  if (rows == 0) return 0;
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(bias_act_fwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const bf16_t*)y, (const bf16_t*)bias, (bf16_t*)out, nvec, N, act);
+    hipLaunchKernelGGL(bias_act_fwd_kernel<bf16_t>, grid, dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)y, (const bf16_t*)bias, (bf16_t*)out, rows, N, act);
   else
-    hipLaunchKernelGGL(bias_act_fwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const float*)y, (const float*)bias, (float*)out, nvec, N, act);
+    hipLaunchKernelGGL(bias_act_fwd_kernel<float>, grid, dim3(EW_THREADS), 0, s,
+                       (const float*)y, (const float*)bias, (float*)out, rows, N, act);
   return 0;
 }
 
 int launch_bias_act_bwd(const void* dout, const void* y, const void* bias, void* dy,
                         float* partial, int nblk_rows, int64_t rows, int N, int act, int dt,
                         hipStream_t s) {
-  if (N % 4) return -2;
-  dim3 grid((N / 4 + EW_THREADS - 1) / EW_THREADS, nblk_rows);
+  if (N % 8) return -2;
+  dim3 grid((N + COLS_PER_BLOCK - 1) / COLS_PER_BLOCK, nblk_rows);
   if (dt == DT_BF16)
     hipLaunchKernelGGL(bias_act_bwd_kernel<bf16_t>, grid, dim3(EW_THREADS), 0, s,
                        (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)bias, (bf16_t*)dy,
@@ -355,27 +431,29 @@ int launch_bias_act_bwd(const void* dout, const void* y, const void* bias, void*
 }
 
 int launch_swiglu_fwd(const void* gu, void* out, int64_t rows, int I, int dt, hipStream_t s) {
-  if (I % 4) return -2;
-  const int64_t nvec = rows * I / 4;
+  if (I % 8) return -2;
+  if (rows == 0) return 0;
+  dim3 grid((I + COLS_PER_BLOCK - 1) / COLS_PER_BLOCK, (unsigned)(rows < 8192 ? rows : 8192));
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(swiglu_fwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const bf16_t*)gu, (bf16_t*)out, nvec, I);
+    hipLaunchKernelGGL(swiglu_fwd_kernel<bf16_t>, grid, dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)gu, (bf16_t*)out, rows, I);
   else
-    hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const float*)gu, (float*)out, nvec, I);
+    hipLaunchKernelGGL(swiglu_fwd_kernel<float>, grid, dim3(EW_THREADS), 0, s,
+                       (const float*)gu, (float*)out, rows, I);
   return 0;
 }
 
 int launch_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, int I, int dt,
                       hipStream_t s) {
-  if (I % 4) return -2;
-  const int64_t nvec = rows * I / 4;
+  if (I % 8) return -2;
+  if (rows == 0) return 0;
+  dim3 grid((I + COLS_PER_BLOCK - 1) / COLS_PER_BLOCK, (unsigned)(rows < 8192 ? rows : 8192));
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(swiglu_bwd_kernel<bf16_t>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, nvec, I);
+    hipLaunchKernelGGL(swiglu_bwd_kernel<bf16_t>, grid, dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, rows, I);
   else
-    hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(ew_grid(nvec)), dim3(EW_THREADS), 0, s,
-                       (const float*)dout, (const float*)gu, (float*)dgu, nvec, I);
+    hipLaunchKernelGGL(swiglu_bwd_kernel<float>, grid, dim3(EW_THREADS), 0, s,
+                       (const float*)dout, (const float*)gu, (float*)dgu, rows, I);
   return 0;
 }
 
@@ -466,6 +544,46 @@ int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* 
     hipLaunchKernelGGL(adamw_kernel<float>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, master,
                        (const float*)grad, m, v, pb, pf, b1, b2, eps, step_size, decay_mul,
                        denom_scale, hf, grad_scale, n);
+  return 0;
+}
+
+int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int param_dt,
+                    const void* const* grads, const int64_t* offs, const int64_t* numels,
+                    int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
+                    int step, int mode, float grad_scale, hipStream_t s) {
+  const double bc1 = 1.0 - __builtin_pow((double)b1, step);
+  const double bc2 = 1.0 - __builtin_pow((double)b2, step);
+  const int hf = mode == 0;
+  const float step_size = hf ? (float)(lr * __builtin_sqrt(bc2) / bc1) : (float)(lr / bc1);
+  const float decay_mul = 1.f - lr * wd;
+  const float denom_scale = hf ? 1.f : (float)(1.0 / __builtin_sqrt(bc2));
+  bf16_t* pb = param_dt == DT_BF16 ? (bf16_t*)param_out : nullptr;
+  float* pf = param_dt == DT_F32 ? (float*)param_out : nullptr;
+  const int esz = grad_dt == DT_BF16 ? 2 : 4;
+  constexpr int64_t CHUNK = 8192;
+  for (int g0 = 0; g0 < ntens; g0 += MT_MAX) {
+    MTArgs a{};
+    a.n = ntens - g0 < MT_MAX ? ntens - g0 : MT_MAX;
+    a.start[0] = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.g[i] = grads[g0 + i];
+      a.off[i] = offs[g0 + i];
+      a.numel[i] = numels[g0 + i];
+      a.start[i + 1] = a.start[i] + (numels[g0 + i] + 3) / 4 * 4;
+      a.aligned[i] = (((uintptr_t)grads[g0 + i]) % (4 * esz) == 0) && (offs[g0 + i] % 4 == 0);
+    }
+    const int64_t total = a.start[a.n];
+    if (total == 0) continue;
+    const unsigned grid = (unsigned)((total + CHUNK - 1) / CHUNK);
+    if (grad_dt == DT_BF16)
+      hipLaunchKernelGGL(adamw_mt_kernel<bf16_t>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
+                         pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
+                         grad_scale);
+    else
+      hipLaunchKernelGGL(adamw_mt_kernel<float>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
+                         pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
+                         grad_scale);
+  }
   return 0;
 }
 

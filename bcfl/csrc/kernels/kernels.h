@@ -19,6 +19,9 @@ int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const f
                      uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s);
 int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,
                   hipStream_t s);
+// reduce planes 0..2 of partial[nblk][3][H] into out0..2 (nullptr = skip) in one launch
+int launch_colsum3(const float* partial, int nblk, int H, void* out0, void* out1, void* out2,
+                   int dt0, int dt1, int dt2, hipStream_t s);
 int launch_emb_ln_fwd(const int* ids, const int* pos, const int* tt, const void* word,
                       const void* posw, const void* typew, const void* gamma, const void* beta,
                       void* out, void* z, float* mean, float* rstd, int T, int H, float eps,
@@ -52,6 +55,10 @@ int launch_delta_encode(const float* x, float* ref, void* out, int out_dt, int64
 int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* v,
                  void* param_out, int param_dt, float lr, float b1, float b2, float eps, float wd,
                  int step, int mode, float grad_scale, int64_t n, hipStream_t s);
+int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int param_dt,
+                    const void* const* grads, const int64_t* offs, const int64_t* numels,
+                    int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
+                    int step, int mode, float grad_scale, hipStream_t s);
 int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
                         float* out, hipStream_t s);
 

@@ -27,16 +27,25 @@ class PackedBatch:
     cu_seqlens: torch.Tensor    # [B+1] int32
     labels: torch.Tensor        # [B] int32
     max_seqlen: int
-    seq_lens: np.ndarray        # host copy of row lengths
-    cu_host: np.ndarray         # host copy of cu_seqlens
+    seq_lens: np.ndarray        # host copy of row lengths (real rows only)
+    cu_host: np.ndarray         # host copy of cu_seqlens (incl. the filler row, if any)
 
     @property
     def batch_size(self) -> int:
+        """Number of REAL rows (a filler row added by :func:`pad_packed` is not counted)."""
         return int(self.seq_lens.shape[0])
+
+    @property
+    def n_seq(self) -> int:
+        return self.batch_size
 
     @property
     def num_tokens(self) -> int:
         return int(self.cu_host[-1])
+
+    @property
+    def real_tokens(self) -> int:
+        return int(self.cu_host[self.batch_size])
 
     def to(self, device, non_blocking: bool = True) -> "PackedBatch":
         return PackedBatch(self.input_ids.to(device, non_blocking=non_blocking),
@@ -44,6 +53,24 @@ class PackedBatch:
                            self.cu_seqlens.to(device, non_blocking=non_blocking),
                            self.labels.to(device, non_blocking=non_blocking),
                            self.max_seqlen, self.seq_lens, self.cu_host)
+
+
+def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
+    """Round the packed token count up to ``multiple`` with ONE filler row appended as its own
+    sequence (attention never mixes it with real rows; pooling/loss only read the real rows).
+    Bucketing T keeps the GEMM shapes (M = T) to a small set, so the BLAS algorithm choice and
+    tuning results are reused batch after batch."""
+    if multiple <= 1:
+        return b
+    T = b.num_tokens
+    P = (-T) % multiple
+    if P == 0:
+        return b
+    ids = torch.cat([b.input_ids, torch.full((P,), pad_id, dtype=torch.int32)])
+    pos = torch.cat([b.position_ids, torch.arange(P, dtype=torch.int32)])
+    cu = np.concatenate([b.cu_host, [T + P]])
+    return PackedBatch(ids, pos, torch.from_numpy(cu.astype(np.int32)), b.labels,
+                       max(b.max_seqlen, P), b.seq_lens, cu)
 
 
 @dataclass
@@ -91,12 +118,13 @@ class ClientLoader:
     """Epoch iterator over one client's rows (train: shuffled like ``DataLoader(shuffle=True)``)."""
 
     def __init__(self, ds: TokenDataset, indices: np.ndarray, batch_size: int = 32,
-                 shuffle: bool = False, seed: int = 0):
+                 shuffle: bool = False, seed: int = 0, pad_multiple: int = 0):
         self.ds = ds
         self.indices = np.asarray(indices, dtype=np.int64)
         self.batch_size = batch_size
         self.shuffle = shuffle
         self.seed = seed
+        self.pad_multiple = pad_multiple
         self.epoch = 0
 
     def __len__(self) -> int:  # number of batches (Flower's num_examples quirk uses this)
@@ -115,7 +143,7 @@ class ClientLoader:
 
     def host_batches(self, epoch: Optional[int] = None) -> List[PackedBatch]:
         order = self._order(epoch)
-        return [make_packed_batch(self.ds, order[i:i + self.batch_size])
+        return [pad_packed(make_packed_batch(self.ds, order[i:i + self.batch_size]), self.pad_multiple)
                 for i in range(0, len(order), self.batch_size)]
 
     def device_batches(self, device, epoch: Optional[int] = None) -> List[PackedBatch]:

@@ -173,15 +173,21 @@ class Federation:
             return np.ceil(ex / self.cfg.batch_size)
         return ex
 
+    @property
+    def pad_multiple(self) -> int:
+        # GPU: bucket T to a multiple of 256 (stable GEMM shapes); CPU: exact shapes
+        return 256 if self.is_cuda else 0
+
     def train_batches(self, c: int, r: int, epoch: int):
         sp = self.partitions(r)[c]
         ld = ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
-                          seed=_cseed(self.cfg.seed, c))
+                          seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple)
         return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
 
     def test_batches(self, c: int, r: int):
         sp = self.partitions(r)[c]
-        return ClientLoader(self.test_ds, sp.test, self.cfg.batch_size).device_batches(self.device)
+        return ClientLoader(self.test_ds, sp.test, self.cfg.batch_size,
+                            pad_multiple=self.pad_multiple).device_batches(self.device)
 
     def global_test_batches(self, r: int):
         idx = global_test_indices(len(self.test_ds), self.cfg.global_test_samples, self.cfg.seed,
@@ -189,7 +195,8 @@ class Federation:
         mine = idx[self.rt.rank::self.rt.world]
         if len(mine) == 0:
             return []
-        return ClientLoader(self.test_ds, mine, self.cfg.batch_size).device_batches(self.device)
+        return ClientLoader(self.test_ds, mine, self.cfg.batch_size,
+                            pad_multiple=self.pad_multiple).device_batches(self.device)
 
     def _activate(self, c: int, master: Optional[torch.Tensor] = None):
         if master is not None:

@@ -56,7 +56,7 @@ class LocalTrainer:
             self.opt.step()
             self.flat.zero_grad()
             loss_acc += loss.detach()
-            tokens += b.num_tokens
+            tokens += b.real_tokens
         return {"loss_sum": loss_acc, "batches": len(batches), "tokens": tokens,
                 "examples": sum(b.batch_size for b in batches)}
 

@@ -104,7 +104,7 @@ class AlbertForSequenceClassification(SeqClassifierBase):
         x = ops.linear(e, self.map_weight, self.map_bias)
         for _ in range(c.num_hidden_layers):
             x = self._layer(x, batch)
-        cls = x.index_select(0, batch.cu_seqlens[:-1].long())
+        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
         pooled = torch.tanh(ops.linear(cls, self.pooler_weight, self.pooler_bias))
         if self.training and c.classifier_dropout_prob > 0:
             pooled = ops.dropout(pooled, c.classifier_dropout_prob, True)

@@ -142,7 +142,7 @@ class BertForSequenceClassification(SeqClassifierBase):
     def forward(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = self.cfg
         x = self.encode(batch, token_type_ids)
-        cls = x.index_select(0, batch.cu_seqlens[:-1].long())
+        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
         pooled = torch.tanh(ops.linear(cls, self.pooler_weight, self.pooler_bias))
         p = c.classifier_dropout if c.classifier_dropout is not None else c.hidden_dropout_prob
         if self.training and p > 0:

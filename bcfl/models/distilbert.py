@@ -120,7 +120,7 @@ class DistilBertForSequenceClassification(SeqClassifierBase):
                                     self.emb_ln_bias, c.layer_norm_eps, c.dropout, self.training)
         for layer in self.layers:
             x = layer(x, batch)
-        cls = x.index_select(0, batch.cu_seqlens[:-1].long())
+        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
         h = torch.relu(ops.linear(cls, self.pre_classifier_weight, self.pre_classifier_bias))
         if self.training and c.seq_classif_dropout > 0:
             h = ops.dropout(h, c.seq_classif_dropout, True)

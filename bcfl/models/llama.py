@@ -137,7 +137,7 @@ class LlamaForSequenceClassification(SeqClassifierBase):
         x = torch.nn.functional.embedding(batch.input_ids.long(), self.embed_tokens)
         for layer in self.layers:
             x = layer(x, batch, self.rope_cos, self.rope_sin)
-        last = x.index_select(0, (batch.cu_seqlens[1:] - 1).long())
+        last = x.index_select(0, (batch.cu_seqlens[1:batch.n_seq + 1] - 1).long())
         last = ops.rmsnorm(last, self.norm, self.cfg.rms_norm_eps)
         return ops.linear(last, self.score_weight)
 

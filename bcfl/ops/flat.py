@@ -31,6 +31,26 @@ def adamw_(master, grad, m, v, step: int, lr: float, beta1: float, beta2: float,
                grad_scale)
 
 
+def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], m, v, step: int,
+                 lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
+                 mode: str = "hf", param_out: Optional[torch.Tensor] = None,
+                 grad_scale: float = 1.0):
+    """AdamW where each gradient is its own tensor (as autograd produced it) and master / m / v /
+    param live in flat buffers at ``offsets``: one multi-tensor launch per <=48 tensors."""
+    if not grads:
+        return
+    if use_native(master):
+        native().adamw_mt(master, m, v, param_out, list(grads), [int(o) for o in offsets],
+                          float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+                          int(step), 0 if mode == "hf" else 1, float(grad_scale))
+        return
+    for g, o in zip(grads, offsets):
+        n = g.numel()
+        po = None if param_out is None or param_out.data_ptr() == master.data_ptr() else param_out[o:o + n]
+        ref.adamw_(master[o:o + n], g.reshape(-1), m[o:o + n], v[o:o + n], step, lr, beta1, beta2,
+                   eps, weight_decay, mode, po, grad_scale)
+
+
 def gossip_mix_(master: torch.Tensor, neighbours: Sequence[torch.Tensor], self_w: float,
                 weights: Sequence[float], param_out: Optional[torch.Tensor] = None):
     """master <- self_w * master + sum_j w_j * neighbour_j (fp32 accumulate; neighbours any dtype)."""

@@ -5,12 +5,13 @@ The reference serialises the model as 201 separate numpy arrays on every exchang
 and loads them back with ``torch.Tensor(v)`` + ``load_state_dict`` (``:164-167``). Here every
 trainable parameter is a VIEW into one flat device buffer (each tensor start aligned to 64
 elements = 128 B for bf16), so FedAvg is one RCCL all-reduce, a gossip exchange is one
-send/recv per peer, AdamW is one kernel, and host round-trips disappear (K12).
+send/recv per peer, AdamW is one multi-tensor kernel, and host round-trips disappear (K12).
 
 Buffers (N = padded element count):
   ``param``  compute dtype (bf16 on MI355X) — what the model reads
   ``master`` fp32 master weights (aliases ``param`` when the compute dtype is fp32)
-  ``grad``   compute dtype; each ``p.grad`` is a view so autograd accumulates in place
+Gradients stay the tensors autograd produces (``p.grad`` is reset to None, so autograd hands
+over its result without an accumulate kernel); the multi-tensor AdamW reads them in place.
 """
 from __future__ import annotations
 
@@ -42,7 +43,6 @@ class FlatParams:
         self.numel = off
         self.num_params = sum(n for _, n, _ in self.slots)
         self.param = torch.zeros(self.numel, dtype=dtype, device=device)
-        self.grad = torch.zeros(self.numel, dtype=dtype, device=device)
         with torch.no_grad():
             for p, (o, n, shp) in zip(params, self.slots):
                 self.param[o:o + n].copy_(p.data.reshape(-1).to(device=device, dtype=dtype))
@@ -59,7 +59,7 @@ class FlatParams:
     def _bind(self):
         for p, (o, n, shp) in zip(self.params, self.slots):
             p.data = self.param[o:o + n].view(shp)
-            p.grad = self.grad[o:o + n].view(shp)
+            p.grad = None
 
     @classmethod
     def from_model(cls, model: nn.Module, device=None, dtype=None) -> "FlatParams":
@@ -68,10 +68,25 @@ class FlatParams:
 
     # ------------------------------------------------------------------------------------
     def zero_grad(self):
-        self.grad.zero_()
-        for p, (o, n, shp) in zip(self.params, self.slots):  # autograd may have replaced .grad
-            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
-                p.grad = self.grad[o:o + n].view(shp)
+        for p in self.params:
+            p.grad = None
+
+    def grads(self):
+        """(grad tensors, flat offsets) of the parameters that received a gradient."""
+        gs, offs = [], []
+        for p, (o, n, shp) in zip(self.params, self.slots):
+            if p.grad is not None:
+                gs.append(p.grad)
+                offs.append(o)
+        return gs, offs
+
+    def flat_grad(self) -> torch.Tensor:
+        """Gradients gathered into one flat fp32 buffer (tests / diagnostics only)."""
+        g = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        for p, (o, n, shp) in zip(self.params, self.slots):
+            if p.grad is not None:
+                g[o:o + n].copy_(p.grad.reshape(-1))
+        return g
 
     @torch.no_grad()
     def sync_param_from_master(self):
@@ -117,9 +132,11 @@ class FlatAdamW:
     def step(self, grad_scale: float = 1.0):
         self.step_count += 1
         f = self.flat
-        ops.adamw_(f.master, f.grad, self.m, self.v, self.step_count, self.lr, self.betas[0],
-                   self.betas[1], self.eps, self.wd, self.mode,
-                   param_out=None if f.master is f.param else f.param, grad_scale=grad_scale)
+        grads, offs = f.grads()
+        ops.adamw_multi_(f.master, grads, offs, self.m, self.v, self.step_count, self.lr,
+                         self.betas[0], self.betas[1], self.eps, self.wd, self.mode,
+                         param_out=None if f.master is f.param else f.param,
+                         grad_scale=grad_scale)
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}

@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel trace + stats of a short bench run (writes gpurun_out/prof/*).
+set -e
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/prof${1:+_$1}
+shift || true
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- \
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 "$@" > "$OUT/bench.log" 2>&1
+tail -3 "$OUT/bench.log"
+find "$OUT" -name '*kernel_stats.csv' | head -1 | xargs -I{} sh -c 'head -30 {}'

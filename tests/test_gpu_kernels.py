@@ -199,6 +199,34 @@ def test_fused_adamw(mode):
     _close(p_out, rm, 1e-2)
 
 
+@pytest.mark.parametrize("mode", ["hf", "torch"])
+def test_multi_tensor_adamw(mode):
+    torch.manual_seed(0)
+    sizes = [768, 2, 3072 * 768, 5, 30522 * 768, 64] + [777] * 45  # > one 40-tensor group
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    master = torch.randn(o, device=DEV)
+    m, v = torch.zeros(o, device=DEV), torch.zeros(o, device=DEV)
+    p_out = torch.zeros(o, device=DEV, dtype=torch.bfloat16)
+    rm, rmm, rvv = master.clone(), m.clone(), v.clone()
+    for t in range(1, 3):
+        grads = [torch.randn(n, device=DEV).bfloat16() for n in sizes]
+        ops.adamw_multi_(master, grads, offs, m, v, t, 1e-3, 0.9, 0.999, 1e-6, 0.01, mode, p_out)
+        for g, of in zip(grads, offs):
+            n = g.numel()
+            ref.adamw_(rm[of:of + n], g.float(), rmm[of:of + n], rvv[of:of + n], t, 1e-3, 0.9,
+                       0.999, 1e-6, 0.01, mode)
+    _close(master, rm, 1e-5, 1e-5)
+    _close(m, rmm, 1e-6, 1e-5)
+    mask = torch.zeros(o, dtype=torch.bool, device=DEV)
+    for n, of in zip(sizes, offs):
+        mask[of:of + n] = True
+    _close(p_out[mask], rm[mask], 1e-2)
+    assert (p_out[~mask] == 0).all()  # padding untouched
+
+
 def test_flat_ops():
     torch.manual_seed(0)
     n = (1 << 18) + 64

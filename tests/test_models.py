@@ -111,6 +111,18 @@ def test_llama_parity_base_weights():
     torch.testing.assert_close(ours, ref, atol=1e-4, rtol=1e-3)
 
 
+@pytest.mark.parametrize("name", ["tiny-bert", "tiny-albert", "tiny-distilbert", "tiny-llama-lora"])
+def test_filler_row_padding_is_invisible(name):
+    from bcfl.data.batching import make_packed_batch, pad_packed
+    m = build_model(name, num_labels=2, seed=0, dtype=torch.float32).eval()
+    ds = load_split("tiny", "train", m.cfg.vocab_size, 128)
+    b = make_packed_batch(ds, np.arange(0, 70, 7))
+    pb = pad_packed(b, 64)
+    assert pb.num_tokens % 64 == 0 and pb.num_tokens > b.num_tokens and pb.batch_size == b.batch_size
+    with torch.no_grad():
+        torch.testing.assert_close(m(pb), m(b), atol=1e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("name,labels,count,params", [
     ("biobert", 41, 201, 108_341_801),
     ("albert-base-v2", 2, 27, 11_685_122),
