@@ -13,14 +13,22 @@
 //          LDS; dV += P^T dO, dK += dS^T Q accumulate in registers over every query (and every
 //          query head of the GQA group) — no atomics, deterministic.
 //
-// MFMA mapping (v_mfma_f32_32x32x16_bf16, see cdna_hip_programming.md §3): the score tile is
-// computed SWAPPED in fwd/dq (S^T = K Q^T: the query is the accumulator COLUMN = lane, so the
-// softmax row statistics are lane-local plus one xor-32 shuffle), and the accumulator feeds the
-// next MFMA directly as its B operand ("accumulator as operand", k-order 16s+8(j>>2)+4h+(j&3)).
-// The A operand of that second product needs the other tensor column-wise: it is read with
-// ds_read_b64_tr_b16 (hardware transpose) from a row-major LDS tile.
+// Pipelining (cdna_hip_programming.md T14 "issue early / write late" + double-buffered LDS): the
+// global loads of tile i+1 are issued into registers BEFORE the MFMAs of tile i, written to the
+// other LDS buffer after them, and ONE barrier per tile publishes it.
+//
+// MFMA mapping (v_mfma_f32_32x32x16_bf16, cdna_hip_programming.md §3): the score tile is computed
+// SWAPPED in fwd/dq (S^T = K Q^T: the query is the accumulator COLUMN = lane, so the softmax row
+// statistics are lane-local plus one xor-32 shuffle), and the accumulator feeds the next MFMA
+// directly as its B operand ("accumulator as operand", k-order 16s+8(j>>2)+4h+(j&3)). The A
+// operand of that second product needs the other tensor column-wise: it is read with
+// ds_read_b64_tr_b16 (hardware transpose, T10) from a row-major LDS tile.
 // LDS row strides: K/Q/dO tiles HD*2+16 B (conflict-free 16-lane ds_read_b128 row reads);
 // V tiles HD*2+64 B (conflict-free 32-lane transposed reads).
+//
+// Softmax VALU trims (d = 64 makes attention VALU-heavy): the softmax scale is folded into the
+// exp2 FMA (max taken on raw scores), key masking runs only on tiles that straddle the sequence
+// end / causal diagonal, and the O rescale is skipped unless some row's running max grew.
 #include <math.h>
 
 #include "common.h"
@@ -74,14 +82,48 @@ __device__ __forceinline__ f32x16_t zero16() {
 // row offset inside a 32x32 accumulator: reg -> row (reg&3) + 8(reg>>2) + 4h
 __device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
 
+// Register-staged loader of two [TILE x HD] row tiles (e.g. K and V) gathered from token rows
+// tok0 + row0 .. of two sources; rows >= L are zero-filled (so masked V rows can never be NaN).
+template <int HD>
+struct Stage2 {
+  static constexpr int CPR = HD / 8;             // 16-byte chunks per row
+  static constexpr int N = TILE * CPR / 256;     // chunks per thread per tensor
+  uint4 a[N], b[N];
+  __device__ __forceinline__ void load(const bf16_t* sa, int rsa, const bf16_t* sb, int rsb,
+                                       int tok0, int row0, int L) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int rr = idx / CPR, c = idx % CPR;
+      const int row = row0 + rr;
+      if (row < L) {
+        a[i] = *reinterpret_cast<const uint4*>(sa + (size_t)(tok0 + row) * rsa + c * 8);
+        b[i] = *reinterpret_cast<const uint4*>(sb + (size_t)(tok0 + row) * rsb + c * 8);
+      } else {
+        a[i] = make_uint4(0, 0, 0, 0);
+        b[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* da, int sda, bf16_t* db, int sdb) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int rr = idx / CPR, c = idx % CPR;
+      *reinterpret_cast<uint4*>(da + rr * sda + c * 8) = a[i];
+      *reinterpret_cast<uint4*>(db + rr * sdb + c * 8) = b[i];
+    }
+  }
+};
+
 // ------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   constexpr int KS = HD + 8;   // K row stride (elements)
   constexpr int VS = HD + 32;  // V row stride
+  constexpr int STG = TILE * (KS + VS);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Vs = Ks + TILE * KS;
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);  // [2 stages][K tile | V tile]
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int tok0 = p.cu[b];
@@ -94,8 +136,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   const int hk = h / (p.nh / p.nkv);
   const int rs = (p.nh + 2 * p.nkv) * HD;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
-  const int koff = p.nh * HD + hk * HD;
-  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+  const bf16_t* ksrc = qkv + p.nh * HD + hk * HD;
+  const bf16_t* vsrc = qkv + (p.nh + p.nkv) * HD + hk * HD;
+  const int kend = p.causal ? min(L, q0 + BLK) : L;
+  const int ntiles = (kend + TILE - 1) / TILE;
+
+  Stage2<HD> stg;
+  stg.load(ksrc, rs, vsrc, rs, tok0, 0, L);
 
   bf16x8_t qf[HD / 16];
   {
@@ -107,85 +154,85 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   f32x16_t o[HD / 32];
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) o[u] = zero16();
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // m: running max in the scaled log2 domain
   const float sl2 = p.scale * LOG2E;
   const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
   const int myq = qw0 + r;
   const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
-  const int kend = p.causal ? min(L, q0 + BLK) : L;
 
-  for (int k0 = 0; k0 < kend; k0 += TILE) {
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
-      const int kr = idx / (HD / 8), c = idx % (HD / 8);
-      const int key = k0 + kr;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (key < L) {
-        const bf16_t* base = qkv + (size_t)(tok0 + key) * rs;
-        kv = *reinterpret_cast<const uint4*>(base + koff + c * 8);
-        vv = *reinterpret_cast<const uint4*>(base + voff + c * 8);
+  stg.store(lds, KS, lds + TILE * KS, VS);
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int k0 = it * TILE;
+    const bool more = it + 1 < ntiles;
+    if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);  // in flight during the MFMAs
+    const bf16_t* Ks = lds + (it & 1) * STG;
+    const bf16_t* Vs = Ks + TILE * KS;
+    if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
+      f32x16_t sacc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sacc[t] = zero16();
+#pragma unroll
+        for (int s = 0; s < HD / 16; ++s)
+          sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
       }
-      *reinterpret_cast<uint4*>(Ks + kr * KS + c * 8) = kv;
-      *reinterpret_cast<uint4*>(Vs + kr * VS + c * 8) = vv;
-    }
-    __syncthreads();
-    if (!active) continue;
-    if (p.causal && k0 > qw0 + ROWS - 1) continue;
-
-    f32x16_t sacc[2];
+      const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
+      if (need_mask) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sacc[t] = zero16();
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s)
-        sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int key = k0 + 32 * t + acc_row(reg, hh);
-        float v = sacc[t][reg] * sl2;
-        if (key >= L || (p.causal && key > myq)) v = -INFINITY;
-        sacc[t][reg] = v;
-        mx = fmaxf(mx, v);
+          for (int reg = 0; reg < 16; ++reg) {
+            const int key = k0 + 32 * t + acc_row(reg, hh);
+            if (key >= L || (p.causal && key > myq)) sacc[t][reg] = -INFINITY;
+          }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
-    l *= alpha;
+      float mx = -INFINITY;
 #pragma unroll
-    for (int u = 0; u < HD / 32; ++u)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) o[u][reg] *= alpha;
-    m = mn;
-
-    bf16x8_t pf[4];
-    float ls = 0.f;
+        for (int reg = 0; reg < 16; ++reg) mx = fmaxf(mx, sacc[t][reg]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+      if (__any(mx > m)) {  // rescale only when some row's max grew (wave-uniform branch)
+        const float mn = fmaxf(m, mx);
+        const float alpha = exp2f(m - mn);
+        l *= alpha;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+        for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        uint32_t hsh = 0;
-        if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+          for (int reg = 0; reg < 16; ++reg) o[u][reg] *= alpha;
+        m = mn;
+      }
+      bf16x8_t pf[4];
+      float ls = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int reg = 4 * g4 + e;
-          float pv = exp2f(sacc[t][reg] - mn);
-          ls += pv;
-          if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv * sd : 0.f;
-          pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          uint32_t hsh = 0;
+          if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int reg = 4 * g4 + e;
+            float pv = exp2f(fmaf(sacc[t][reg], sl2, -m));
+            ls += pv;
+            if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv * sd : 0.f;
+            pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
+          }
         }
-      }
-    l += ls;
+      l += ls;
 #pragma unroll
-    for (int u = 0; u < HD / 32; ++u)
+      for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t a = tr_operand(Vs, VS, 16 * ks + 4 * hh, 32 * u, lane);
-        o[u] = mfma32(a, pf[ks], o[u]);
-      }
+        for (int ks = 0; ks < 4; ++ks)
+          o[u] = mfma32(tr_operand(Vs, VS, 16 * ks + 4 * hh, 32 * u, lane), pf[ks], o[u]);
+    }
+    if (more) {
+      bf16_t* nk = lds + ((it + 1) & 1) * STG;
+      stg.store(nk, KS, nk + TILE * KS, VS);
+    }
+    __syncthreads();
   }
   if (!active) return;
   l += __shfl_xor(l, 32, 64);
@@ -233,9 +280,9 @@ template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
   constexpr int KS = HD + 8;  // K: row reads (S^T) + transposed reads (dQ)
   constexpr int VS = HD + 8;  // V: row reads (dP^T)
+  constexpr int STG = TILE * (KS + VS);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Vs = Ks + TILE * KS;
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int tok0 = p.cu[b];
@@ -249,10 +296,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
   const int rs = (p.nh + 2 * p.nkv) * HD;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
-  const int koff = p.nh * HD + hk * HD;
-  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+  const bf16_t* ksrc = qkv + p.nh * HD + hk * HD;
+  const bf16_t* vsrc = qkv + (p.nh + p.nkv) * HD + hk * HD;
   const int myq = qw0 + r;
   const int qi = min(myq, L - 1);
+  const int kend = p.causal ? min(L, q0 + BLK) : L;
+  const int ntiles = (kend + TILE - 1) / TILE;
+
+  Stage2<HD> stg;
+  stg.load(ksrc, rs, vsrc, rs, tok0, 0, L);
 
   bf16x8_t qf[HD / 16], df[HD / 16];
   {
@@ -272,60 +324,60 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
   const float sl2 = p.scale * LOG2E;
   const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
   const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
-  const int kend = p.causal ? min(L, q0 + BLK) : L;
 
-  for (int k0 = 0; k0 < kend; k0 += TILE) {
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
-      const int kr = idx / (HD / 8), c = idx % (HD / 8);
-      const int key = k0 + kr;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (key < L) {
-        const bf16_t* base = qkv + (size_t)(tok0 + key) * rs;
-        kv = *reinterpret_cast<const uint4*>(base + koff + c * 8);
-        vv = *reinterpret_cast<const uint4*>(base + voff + c * 8);
-      }
-      *reinterpret_cast<uint4*>(Ks + kr * KS + c * 8) = kv;
-      *reinterpret_cast<uint4*>(Vs + kr * VS + c * 8) = vv;
-    }
-    __syncthreads();
-    if (!active) continue;
-    if (p.causal && k0 > qw0 + ROWS - 1) continue;
+  stg.store(lds, KS, lds + TILE * KS, VS);
+  __syncthreads();
 
-    f32x16_t sacc[2], pacc[2];
+  for (int it = 0; it < ntiles; ++it) {
+    const int k0 = it * TILE;
+    const bool more = it + 1 < ntiles;
+    if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);
+    const bf16_t* Ks = lds + (it & 1) * STG;
+    const bf16_t* Vs = Ks + TILE * KS;
+    if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
+      f32x16_t sacc[2], pacc[2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sacc[t] = zero16();
-      pacc[t] = zero16();
+      for (int t = 0; t < 2; ++t) {
+        sacc[t] = zero16();
+        pacc[t] = zero16();
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s) {
-        sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
-        pacc[t] = mfma32(lds_row8(Vs + (32 * t + r) * VS + 16 * s + 8 * hh), df[s], pacc[t]);
-      }
-    }
-    bf16x8_t dsf[4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        uint32_t hsh = 0;
-        if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int reg = 4 * g4 + e;
-          const int key = k0 + 32 * t + acc_row(reg, hh);
-          float pv = exp2f(sacc[t][reg] * sl2 - lse2);
-          if (key >= L || (p.causal && key > myq)) pv = 0.f;
-          float dp = pacc[t][reg];
-          if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp * sd : 0.f;
-          dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
+        for (int s = 0; s < HD / 16; ++s) {
+          sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
+          pacc[t] = mfma32(lds_row8(Vs + (32 * t + r) * VS + 16 * s + 8 * hh), df[s], pacc[t]);
         }
       }
+      const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
+      bf16x8_t dsf[4];
 #pragma unroll
-    for (int u = 0; u < HD / 32; ++u)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        dq[u] = mfma32(tr_operand(Ks, KS, 16 * ks + 4 * hh, 32 * u, lane), dsf[ks], dq[u]);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          uint32_t hsh = 0;
+          if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int reg = 4 * g4 + e;
+            float pv = exp2f(fmaf(sacc[t][reg], sl2, -lse2));
+            if (need_mask) {
+              const int key = k0 + 32 * t + acc_row(reg, hh);
+              if (key >= L || (p.causal && key > myq)) pv = 0.f;
+            }
+            float dp = pacc[t][reg];
+            if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp * sd : 0.f;
+            dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
+          }
+        }
+#pragma unroll
+      for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          dq[u] = mfma32(tr_operand(Ks, KS, 16 * ks + 4 * hh, 32 * u, lane), dsf[ks], dq[u]);
+    }
+    if (more) {
+      bf16_t* nk = lds + ((it + 1) & 1) * STG;
+      stg.store(nk, KS, nk + TILE * KS, VS);
+    }
+    __syncthreads();
   }
   if (!active || myq >= L) return;
   bf16_t* dst = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + myq) * rs + h * HD;
@@ -343,11 +395,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   constexpr int QS = HD + 8;  // Q / dO tiles: row reads + transposed reads
+  constexpr int STG = TILE * 2 * QS + 2 * TILE * 2;  // Q | dO | lse, delta (fp32 = 2 bf16 slots)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Ds = Qs + TILE * QS;
-  float* lse_s = reinterpret_cast<float*>(Ds + TILE * QS);
-  float* dl_s = lse_s + TILE;
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   const int b = blockIdx.z, hk = blockIdx.y;
   const int tok0 = p.cu[b];
@@ -365,6 +415,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   const int voff = (p.nh + p.nkv) * HD + hk * HD;
   const int mykey = kw0 + r;
   const int ki = min(mykey, L - 1);
+  const int qstart = p.causal ? (kb0 / TILE) * TILE : 0;
+  const int nqt = (L - qstart + TILE - 1) / TILE;  // q tiles per head
+  const int ntiles = nqt * grp;
+
+  Stage2<HD> stg;
+  float ls_r = 0.f, dl_r = 0.f;  // lse / delta of row threadIdx.x (threads < TILE)
+  auto issue = [&](int it) {
+    const int hq = hk * grp + it / nqt;
+    const int q0 = qstart + (it % nqt) * TILE;
+    stg.load(qkv + hq * HD, rs, dout + hq * HD, p.nh * HD, tok0, q0, L);
+    if (threadIdx.x < TILE) {
+      const int q = q0 + threadIdx.x;
+      ls_r = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E : 0.f;
+      dl_r = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+    bf16_t* Qs = lds + buf * STG;
+    bf16_t* Ds = Qs + TILE * QS;
+    stg.store(Qs, QS, Ds, QS);
+    float* fs = reinterpret_cast<float*>(Ds + TILE * QS);
+    if (threadIdx.x < TILE) {
+      fs[threadIdx.x] = ls_r;
+      fs[TILE + threadIdx.x] = dl_r;
+    }
+  };
+  issue(0);
 
   bf16x8_t kf[HD / 16], vf[HD / 16];
   {
@@ -380,39 +457,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv[u] = zero16(); }
   const float sl2 = p.scale * LOG2E;
   const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
-  const int qstart = p.causal ? (kb0 / TILE) * TILE : 0;
 
-  for (int hq = hk * grp; hq < (hk + 1) * grp; ++hq) {
-    for (int q0 = qstart; q0 < L; q0 += TILE) {
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < TILE * HD / 8; idx += 256) {
-        const int qr = idx / (HD / 8), c = idx % (HD / 8);
-        const int q = q0 + qr;
-        uint4 qv = make_uint4(0, 0, 0, 0), dv_ = make_uint4(0, 0, 0, 0);
-        if (q < L) {
-          qv = *reinterpret_cast<const uint4*>(qkv + (size_t)(tok0 + q) * rs + hq * HD + c * 8);
-          dv_ = *reinterpret_cast<const uint4*>(dout + (size_t)(tok0 + q) * p.nh * HD + hq * HD + c * 8);
-        }
-        *reinterpret_cast<uint4*>(Qs + qr * QS + c * 8) = qv;
-        *reinterpret_cast<uint4*>(Ds + qr * QS + c * 8) = dv_;
-      }
-      if (threadIdx.x < TILE) {
-        const int q = q0 + threadIdx.x;
-        lse_s[threadIdx.x] = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E : 0.f;
-        dl_s[threadIdx.x] = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] : 0.f;
-      }
-      __syncthreads();
-      if (!active) continue;
+  commit(0);
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int hq = hk * grp + it / nqt;
+    const int q0 = qstart + (it % nqt) * TILE;
+    const bool more = it + 1 < ntiles;
+    if (more) issue(it + 1);
+    const bf16_t* Qs = lds + (it & 1) * STG;
+    const bf16_t* Ds = Qs + TILE * QS;
+    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE * QS);
+    const float* dl_s = lse_s + TILE;
+    if (active) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int qt0 = q0 + 32 * t;
         if (p.causal && qt0 + 31 < kw0) continue;  // every query of the subtile precedes my keys
+        if (qt0 >= L) continue;
         f32x16_t sacc = zero16(), pacc = zero16();
 #pragma unroll
         for (int s = 0; s < HD / 16; ++s) {
           sacc = mfma32(lds_row8(Qs + (32 * t + r) * QS + 16 * s + 8 * hh), kf[s], sacc);
           pacc = mfma32(lds_row8(Ds + (32 * t + r) * QS + 16 * s + 8 * hh), vf[s], pacc);
         }
+        const bool need_mask = (qt0 + 32 > L) || (p.causal && qt0 < kw0 + ROWS);
         bf16x8_t pf[2], dsf[2];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -424,8 +494,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
           for (int e = 0; e < 4; ++e) {
             const int reg = 4 * g4 + e;
             const int q = q0 + ql + e;
-            float pv = exp2f(sacc[reg] * sl2 - lsv[e]);
-            if (q >= L || (p.causal && mykey > q)) pv = 0.f;
+            float pv = exp2f(fmaf(sacc[reg], sl2, -lsv[e]));
+            if (need_mask && (q >= L || (p.causal && mykey > q))) pv = 0.f;
             float pd = pv, dp = pacc[reg];
             if (p.p8) {
               const uint32_t idx = (uint32_t)((tok0 + q) * p.nh + hq) * (uint32_t)DROP_STRIDE + (uint32_t)mykey;
@@ -446,6 +516,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
           }
       }
     }
+    if (more) commit((it + 1) & 1);
+    __syncthreads();
   }
   if (!active || mykey >= L) return;
   bf16_t* drow = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + mykey) * rs;
@@ -466,7 +538,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
 template <int HD>
 void fwd_hd(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.max_s + BLK - 1) / BLK, p.nh, p.B);
-  const size_t lds = (size_t)TILE * ((HD + 8) + (HD + 32)) * 2;
+  const size_t lds = (size_t)2 * TILE * ((HD + 8) + (HD + 32)) * 2;
   hipLaunchKernelGGL(attn_fwd_kernel<HD>, grid, dim3(256), lds, s, p);
 }
 
@@ -479,9 +551,9 @@ void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
   const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
   hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
                      dim3(256), 0, s, dout, out, p.delta, rows);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)TILE * 2 * (HD + 8) * 2, s, p);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)2 * TILE * 2 * (HD + 8) * 2, s, p);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, gk, dim3(256),
-                     (size_t)TILE * 2 * (HD + 8) * 2 + 2 * TILE * 4, s, p);
+                     (size_t)2 * (TILE * 2 * (HD + 8) + 2 * TILE * 2) * 2, s, p);
 }
 
 int launch_attn_fwd(const AttnParams& p, hipStream_t s) {
