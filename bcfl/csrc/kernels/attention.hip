@@ -23,8 +23,8 @@
 // directly as its B operand ("accumulator as operand", k-order 16s+8(j>>2)+4h+(j&3)). The A
 // operand of that second product needs the other tensor column-wise: it is read with
 // ds_read_b64_tr_b16 (hardware transpose, T10) from a row-major LDS tile.
-// LDS row strides: K/Q/dO tiles HD*2+16 B (conflict-free 16-lane ds_read_b128 row reads);
-// V tiles HD*2+64 B (conflict-free 32-lane transposed reads).
+// LDS tiles are unpadded and 16-B-unit XOR-swizzled so both row reads and transposed reads are
+// bank-conflict-free (see swz()).
 //
 // Softmax VALU trims (d = 64 makes attention VALU-heavy): the softmax scale is folded into the
 // exp2 FMA (max taken on raw scores), key masking runs only on tiles that straddle the sequence
@@ -47,6 +47,16 @@ constexpr float LN2 = 0.6931471805599453f;
 
 typedef __attribute__((ext_vector_type(8))) short s16x8_t;
 
+// raw v_exp_f32: softmax arguments are <= 0 and a flushed denormal result is harmless, so skip
+// exp2f's denormal range-reduction (cmp + 2 cndmask + add + ldexp per element).
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// broadcast lane (quad base + E) of each 4-lane quad (DPP quad_perm, no LDS round trip)
+template <int E>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, E | (E << 2) | (E << 4) | (E << 6), 0xf, 0xf, false);
+}
+
 __device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -59,15 +69,57 @@ __device__ __forceinline__ s16x4_t tr4(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
-// A operand holding X[k][r] for k = kb + {0..3} (elements 0..3) and kb + 8 + {0..3} (4..7), where
-// X is a row-major LDS tile [k][col] with row stride `stride`, lane column r = col0 + (lane & 31).
-// Per 16-lane group g: block rows kb..kb+3, columns col0 + 16(g&1) .. +15.
-__device__ __forceinline__ bf16x8_t tr_operand(const bf16_t* tile, int stride, int kb, int col0,
-                                               int lane) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3;
-  const bf16_t* p0 = tile + (kb + q) * stride + col0 + 16 * (g & 1) + 4 * pc;
-  const s16x4_t lo = tr4(p0);
-  const s16x4_t hi = tr4(p0 + 8 * stride);
+// ---- LDS tile layout -----------------------------------------------------------------------
+// Every staged tile is [TILE rows][HD] bf16 with NO padding; 16-byte units of a row are XOR-
+// swizzled: element (row, col) lives at row*HD + ((col/8) ^ swz(row))*8 + col%8. One layout serves
+// both access kinds (MI355X_MICROARCH.md §LDS bank rules):
+//   * row reads (ds_read_b128, lane = row, 16-lane groups {0-3,12-15,20-27}/{4-11,16-19,28-31}):
+//     the 16 rows of a group land on 16 distinct 16-B slots of the 256-B bank row;
+//   * transposed reads (ds_read_b64_tr_b16, 32-lane halves read 4 consecutive rows x 64 B): the
+//     4 rows land on disjoint quarters of the bank row.
+// The padded strides this replaces were conflict-free for one kind only (2-way on the other).
+// swz(row) depends on row bits 0..3 only, so it is invariant under the multiple-of-16 row offsets
+// the loops add: all lane-dependent addressing is precomputed once (TileOffsets).
+template <int HD>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (HD == 32) {
+    return (row >> 2) & 3;
+  } else if constexpr (HD == 64) {
+    const int a = (row >> 1) & 7;
+    return ((a & 1) << 2) | (((a >> 2) & 1) << 1) | ((a >> 1) & 1);
+  } else {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+  }
+}
+template <int HD>
+__device__ __forceinline__ int swz_off(int row, int unit) {
+  return row * HD + ((unit ^ swz<HD>(row)) << 3);
+}
+
+template <int HD>
+struct TileOffsets {
+  // row reads: MFMA operand of row (lane & 31) [+32t], k-unit 2s + hh
+  int row[HD / 16];
+  // transposed reads (A operand of the second product, X[k][col] for k = kb + {0..3, 8..11}):
+  // per 16-lane group g, rows kb + 4hh + ((lane & 15) >> 2) [+8 for the high half], columns
+  // 32u + 16(g & 1) + 4(lane & 3); the multiple-of-16 part of kb is added by the caller.
+  int tr[HD / 32][2];
+  __device__ __forceinline__ void init(int lane) {
+    const int r = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) row[s] = swz_off<HD>(r, 2 * s + hh);
+    const int g = (lane >> 4) & 1, q = (lane & 15) >> 2, pc = lane & 3;
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+        tr[u][hi] = swz_off<HD>(4 * hh + q + 8 * hi, 4 * u + 2 * g + (pc >> 1)) + 4 * (pc & 1);
+  }
+};
+
+__device__ __forceinline__ bf16x8_t tr_operand(const bf16_t* tile, int off_lo, int off_hi) {
+  const s16x4_t lo = tr4(tile + off_lo);
+  const s16x4_t hi = tr4(tile + off_hi);
   const s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8_t, v);
 }
@@ -105,13 +157,13 @@ struct Stage2 {
       }
     }
   }
-  __device__ __forceinline__ void store(bf16_t* da, int sda, bf16_t* db, int sdb) const {
+  __device__ __forceinline__ void store(bf16_t* da, bf16_t* db) const {  // swizzled tiles
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int idx = threadIdx.x + 256 * i;
-      const int rr = idx / CPR, c = idx % CPR;
-      *reinterpret_cast<uint4*>(da + rr * sda + c * 8) = a[i];
-      *reinterpret_cast<uint4*>(db + rr * sdb + c * 8) = b[i];
+      const int o = swz_off<HD>(idx / CPR, idx % CPR);
+      *reinterpret_cast<uint4*>(da + o) = a[i];
+      *reinterpret_cast<uint4*>(db + o) = b[i];
     }
   }
 };
@@ -119,9 +171,7 @@ struct Stage2 {
 // ------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
-  constexpr int KS = HD + 8;   // K row stride (elements)
-  constexpr int VS = HD + 32;  // V row stride
-  constexpr int STG = TILE * (KS + VS);
+  constexpr int STG = 2 * TILE * HD;  // K tile | V tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);  // [2 stages][K tile | V tile]
 
@@ -160,7 +210,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   const int myq = qw0 + r;
   const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
 
-  stg.store(lds, KS, lds + TILE * KS, VS);
+  TileOffsets<HD> to;
+  to.init(lane);
+  stg.store(lds, lds + TILE * HD);
   __syncthreads();
 
   for (int it = 0; it < ntiles; ++it) {
@@ -168,7 +220,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
     const bool more = it + 1 < ntiles;
     if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);  // in flight during the MFMAs
     const bf16_t* Ks = lds + (it & 1) * STG;
-    const bf16_t* Vs = Ks + TILE * KS;
+    const bf16_t* Vs = Ks + TILE * HD;
     if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
       f32x16_t sacc[2];
 #pragma unroll
@@ -176,7 +228,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
         sacc[t] = zero16();
 #pragma unroll
         for (int s = 0; s < HD / 16; ++s)
-          sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
+          sacc[t] = mfma32(lds_row8(Ks + 32 * t * HD + to.row[s]), qf[s], sacc[t]);
       }
       const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
       if (need_mask) {
@@ -196,7 +248,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
       if (__any(mx > m)) {  // rescale only when some row's max grew (wave-uniform branch)
         const float mn = fmaxf(m, mx);
-        const float alpha = exp2f(m - mn);
+        const float alpha = fexp2(m - mn);
         l *= alpha;
 #pragma unroll
         for (int u = 0; u < HD / 32; ++u)
@@ -215,9 +267,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int reg = 4 * g4 + e;
-            float pv = exp2f(fmaf(sacc[t][reg], sl2, -m));
+            float pv = fexp2(fmaf(sacc[t][reg], sl2, -m));
             ls += pv;
-            if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv * sd : 0.f;
+            if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv : 0.f;  // 1/(1-p) applied at the end
             pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
           }
         }
@@ -226,18 +278,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
       for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
-          o[u] = mfma32(tr_operand(Vs, VS, 16 * ks + 4 * hh, 32 * u, lane), pf[ks], o[u]);
+          o[u] = mfma32(tr_operand(Vs + 16 * ks * HD, to.tr[u][0], to.tr[u][1]), pf[ks], o[u]);
     }
     if (more) {
       bf16_t* nk = lds + ((it + 1) & 1) * STG;
-      stg.store(nk, KS, nk + TILE * KS, VS);
+      stg.store(nk, nk + TILE * HD);
     }
     __syncthreads();
   }
   if (!active) return;
   l += __shfl_xor(l, 32, 64);
   if (myq >= L) return;
-  const float inv = 1.f / l;
+  const float inv = sd / l;
   bf16_t* orow = reinterpret_cast<bf16_t*>(p.out) + (size_t)(tok0 + myq) * p.nh * HD + h * HD;
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u)
@@ -278,9 +330,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 // ------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
-  constexpr int KS = HD + 8;  // K: row reads (S^T) + transposed reads (dQ)
-  constexpr int VS = HD + 8;  // V: row reads (dP^T)
-  constexpr int STG = TILE * (KS + VS);
+  constexpr int STG = 2 * TILE * HD;  // K tile (row reads for S^T, transposed for dQ) | V tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
@@ -316,16 +366,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
       df[s] = *reinterpret_cast<const bf16x8_t*>(drow_ + 16 * s + 8 * hh);
     }
   }
-  const float lse2 = p.lse[(size_t)(tok0 + qi) * p.nh + h] * LOG2E;
-  const float dlt = p.delta[(size_t)(tok0 + qi) * p.nh + h];
+  // dropout's 1/(1-p) is folded into P (lse shifted by log2 sd) and delta (divided by sd):
+  // dS = P sd (keep dP - delta / sd) — no per-element scale multiply.
+  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const float lse2 = p.lse[(size_t)(tok0 + qi) * p.nh + h] * LOG2E - log2f(sd);
+  const float dlt = p.delta[(size_t)(tok0 + qi) * p.nh + h] / sd;
   f32x16_t dq[HD / 32];
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) dq[u] = zero16();
   const float sl2 = p.scale * LOG2E;
-  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
   const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
 
-  stg.store(lds, KS, lds + TILE * KS, VS);
+  TileOffsets<HD> to;
+  to.init(lane);
+  stg.store(lds, lds + TILE * HD);
   __syncthreads();
 
   for (int it = 0; it < ntiles; ++it) {
@@ -333,7 +387,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
     const bool more = it + 1 < ntiles;
     if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);
     const bf16_t* Ks = lds + (it & 1) * STG;
-    const bf16_t* Vs = Ks + TILE * KS;
+    const bf16_t* Vs = Ks + TILE * HD;
     if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
       f32x16_t sacc[2], pacc[2];
 #pragma unroll
@@ -342,8 +396,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
         pacc[t] = zero16();
 #pragma unroll
         for (int s = 0; s < HD / 16; ++s) {
-          sacc[t] = mfma32(lds_row8(Ks + (32 * t + r) * KS + 16 * s + 8 * hh), qf[s], sacc[t]);
-          pacc[t] = mfma32(lds_row8(Vs + (32 * t + r) * VS + 16 * s + 8 * hh), df[s], pacc[t]);
+          sacc[t] = mfma32(lds_row8(Ks + 32 * t * HD + to.row[s]), qf[s], sacc[t]);
+          pacc[t] = mfma32(lds_row8(Vs + 32 * t * HD + to.row[s]), df[s], pacc[t]);
         }
       }
       const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
@@ -357,13 +411,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int reg = 4 * g4 + e;
-            float pv = exp2f(fmaf(sacc[t][reg], sl2, -lse2));
+            float pv = fexp2(fmaf(sacc[t][reg], sl2, -lse2));
             if (need_mask) {
               const int key = k0 + 32 * t + acc_row(reg, hh);
               if (key >= L || (p.causal && key > myq)) pv = 0.f;
             }
             float dp = pacc[t][reg];
-            if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp * sd : 0.f;
+            if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp : 0.f;
             dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
           }
         }
@@ -371,11 +425,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
       for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
-          dq[u] = mfma32(tr_operand(Ks, KS, 16 * ks + 4 * hh, 32 * u, lane), dsf[ks], dq[u]);
+          dq[u] = mfma32(tr_operand(Ks + 16 * ks * HD, to.tr[u][0], to.tr[u][1]), dsf[ks], dq[u]);
     }
     if (more) {
       bf16_t* nk = lds + ((it + 1) & 1) * STG;
-      stg.store(nk, KS, nk + TILE * KS, VS);
+      stg.store(nk, nk + TILE * HD);
     }
     __syncthreads();
   }
@@ -394,8 +448,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 // ------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
-  constexpr int QS = HD + 8;  // Q / dO tiles: row reads + transposed reads
-  constexpr int STG = TILE * 2 * QS + 2 * TILE * 2;  // Q | dO | lse, delta (fp32 = 2 bf16 slots)
+  constexpr int STG = 2 * TILE * HD + 2 * TILE * 2;  // Q | dO | lse, delta (fp32 = 2 bf16 slots)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
@@ -419,6 +472,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   const int nqt = (L - qstart + TILE - 1) / TILE;  // q tiles per head
   const int ntiles = nqt * grp;
 
+  // dropout scale folded into the staged lse / delta exactly as in the dq kernel
+  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const float lsd = log2f(sd), isd = 1.f / sd;
   Stage2<HD> stg;
   float ls_r = 0.f, dl_r = 0.f;  // lse / delta of row threadIdx.x (threads < TILE)
   auto issue = [&](int it) {
@@ -427,15 +483,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
     stg.load(qkv + hq * HD, rs, dout + hq * HD, p.nh * HD, tok0, q0, L);
     if (threadIdx.x < TILE) {
       const int q = q0 + threadIdx.x;
-      ls_r = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E : 0.f;
-      dl_r = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] : 0.f;
+      ls_r = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E - lsd : 0.f;
+      dl_r = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] * isd : 0.f;
     }
   };
   auto commit = [&](int buf) {
     bf16_t* Qs = lds + buf * STG;
-    bf16_t* Ds = Qs + TILE * QS;
-    stg.store(Qs, QS, Ds, QS);
-    float* fs = reinterpret_cast<float*>(Ds + TILE * QS);
+    bf16_t* Ds = Qs + TILE * HD;
+    stg.store(Qs, Ds);
+    float* fs = reinterpret_cast<float*>(Ds + TILE * HD);
     if (threadIdx.x < TILE) {
       fs[threadIdx.x] = ls_r;
       fs[TILE + threadIdx.x] = dl_r;
@@ -456,8 +512,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv[u] = zero16(); }
   const float sl2 = p.scale * LOG2E;
-  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  // dropout keep bits: element (q, key) uses byte key&3 of hash((q*nh+hq)*2048 + key/4); the 4
+  // lanes of a quad (keys 4j..4j+3) share those hashes, so lane j of the quad hashes query e=j and
+  // the others receive it by DPP quad broadcast (4x fewer quarter-rate v_mul_lo_u32 chains).
+  const uint32_t kq = (uint32_t)mykey >> 2, bsh = 8u * (uint32_t)(r & 3);
 
+  TileOffsets<HD> to;
+  to.init(lane);
   commit(0);
   __syncthreads();
 
@@ -467,8 +528,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
     const bool more = it + 1 < ntiles;
     if (more) issue(it + 1);
     const bf16_t* Qs = lds + (it & 1) * STG;
-    const bf16_t* Ds = Qs + TILE * QS;
-    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE * QS);
+    const bf16_t* Ds = Qs + TILE * HD;
+    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE * HD);
     const float* dl_s = lse_s + TILE;
     if (active) {
 #pragma unroll
@@ -479,8 +540,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
         f32x16_t sacc = zero16(), pacc = zero16();
 #pragma unroll
         for (int s = 0; s < HD / 16; ++s) {
-          sacc = mfma32(lds_row8(Qs + (32 * t + r) * QS + 16 * s + 8 * hh), kf[s], sacc);
-          pacc = mfma32(lds_row8(Ds + (32 * t + r) * QS + 16 * s + 8 * hh), vf[s], pacc);
+          sacc = mfma32(lds_row8(Qs + 32 * t * HD + to.row[s]), kf[s], sacc);
+          pacc = mfma32(lds_row8(Ds + 32 * t * HD + to.row[s]), vf[s], pacc);
         }
         const bool need_mask = (qt0 + 32 > L) || (p.causal && qt0 < kw0 + ROWS);
         bf16x8_t pf[2], dsf[2];
@@ -490,18 +551,27 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
           const float4 ls4 = *reinterpret_cast<const float4*>(lse_s + ql);
           const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + ql);
           const float lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+          uint32_t hq4[4] = {0u, 0u, 0u, 0u};
+          if (p.p8) {
+            const uint32_t mine = hash32(
+                (((uint32_t)((tok0 + q0 + ql + (r & 3)) * p.nh + hq) * (uint32_t)DROP_STRIDE) >> 2) + kq,
+                p.ka, p.kb);
+            hq4[0] = quad_bcast<0>(mine);
+            hq4[1] = quad_bcast<1>(mine);
+            hq4[2] = quad_bcast<2>(mine);
+            hq4[3] = quad_bcast<3>(mine);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int reg = 4 * g4 + e;
             const int q = q0 + ql + e;
-            float pv = exp2f(fmaf(sacc[reg], sl2, -lsv[e]));
+            float pv = fexp2(fmaf(sacc[reg], sl2, -lsv[e]));  // = P / (1 - p)
             if (need_mask && (q >= L || (p.causal && mykey > q))) pv = 0.f;
             float pd = pv, dp = pacc[reg];
             if (p.p8) {
-              const uint32_t idx = (uint32_t)((tok0 + q) * p.nh + hq) * (uint32_t)DROP_STRIDE + (uint32_t)mykey;
-              const bool keep = keep_elem(idx, p.p8, p.ka, p.kb);
-              pd = keep ? pv * sd : 0.f;
-              dp = keep ? dp * sd : 0.f;
+              const bool keep = ((hq4[e] >> bsh) & 0xffu) >= p.p8;
+              pd = keep ? pv : 0.f;
+              dp = keep ? dp : 0.f;
             }
             pf[reg >> 3][reg & 7] = (__bf16)pd;
             dsf[reg >> 3][reg & 7] = (__bf16)(pv * (dp - dlv[e]));
@@ -511,8 +581,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
         for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
-            dv[u] = mfma32(tr_operand(Ds, QS, 32 * t + 16 * s2 + 4 * hh, 32 * u, lane), pf[s2], dv[u]);
-            dk[u] = mfma32(tr_operand(Qs, QS, 32 * t + 16 * s2 + 4 * hh, 32 * u, lane), dsf[s2], dk[u]);
+            const int kb = (32 * t + 16 * s2) * HD;
+            dv[u] = mfma32(tr_operand(Ds + kb, to.tr[u][0], to.tr[u][1]), pf[s2], dv[u]);
+            dk[u] = mfma32(tr_operand(Qs + kb, to.tr[u][0], to.tr[u][1]), dsf[s2], dk[u]);
           }
       }
     }
@@ -538,7 +609,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
 template <int HD>
 void fwd_hd(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.max_s + BLK - 1) / BLK, p.nh, p.B);
-  const size_t lds = (size_t)2 * TILE * ((HD + 8) + (HD + 32)) * 2;
+  const size_t lds = (size_t)2 * 2 * TILE * HD * 2;
   hipLaunchKernelGGL(attn_fwd_kernel<HD>, grid, dim3(256), lds, s, p);
 }
 
@@ -551,9 +622,9 @@ void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
   const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
   hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
                      dim3(256), 0, s, dout, out, p.delta, rows);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)2 * TILE * 2 * (HD + 8) * 2, s, p);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)2 * 2 * TILE * HD * 2, s, p);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, gk, dim3(256),
-                     (size_t)2 * (TILE * 2 * (HD + 8) + 2 * TILE * 2) * 2, s, p);
+                     (size_t)2 * (2 * TILE * HD + 2 * TILE * 2) * 2, s, p);
 }
 
 int launch_attn_fwd(const AttnParams& p, hipStream_t s) {

@@ -19,16 +19,19 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// round-to-nearest-even f32 -> bf16 (NaN kept quiet)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// round-to-nearest-even f32 -> bf16: gfx950 has v_cvt_pk_bf16_f32 (RNE, NaN quieted), one
+// instruction per pair instead of the ~7-op integer rounding sequence.
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  bf16x2_t v;
+  v[0] = (__bf16)a;
+  v[1] = (__bf16)b;
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // generic element load/store for float / bf16 buffers
