@@ -425,12 +425,34 @@ Tensor sha256_merkle(Tensor leaves) {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------------
+// dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
+Tensor wgrad(Tensor g, Tensor x) {
+  TORCH_CHECK(g.is_cuda() && x.is_cuda(), "wgrad: GPU tensors required");
+  TORCH_CHECK(g.dim() == 2 && x.dim() == 2 && g.size(0) == x.size(0), "wgrad: g [M,N], x [M,K]");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16");
+  TORCH_CHECK(g.stride(1) == 1 && x.stride(1) == 1, "wgrad: rows must be contiguous");
+  TORCH_CHECK(g.stride(0) % 8 == 0 && x.stride(0) % 8 == 0, "wgrad: 16-byte aligned rows");
+  const int M = g.size(0), N = g.size(1), K = x.size(1);
+  int Mc = 0;
+  const int S = bcfl::wgrad_splits(M, N, K, &Mc);
+  TORCH_CHECK(S >= 1, "wgrad: N and K must be multiples of 128");
+  auto out = torch::empty({N, K}, g.options());
+  Tensor part;
+  if (S > 1) part = torch::empty({S, N, K}, g.options().dtype(torch::kFloat));
+  bcfl::WgradParams p{g.data_ptr(), x.data_ptr(), S > 1 ? part.data_ptr<float>() : nullptr,
+                      out.data_ptr(), g.stride(0), x.stride(0), K, M, N, K, S, Mc};
+  check_rc(bcfl::launch_wgrad(p, stream()), "wgrad");
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "bcfl gfx950 (CDNA4) kernels";
   m.def("bdaln_fwd", &bdaln_fwd);
   m.def("bdaln_bwd", &bdaln_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("wgrad", &wgrad);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);

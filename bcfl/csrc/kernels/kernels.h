@@ -68,6 +68,19 @@ int launch_sha256_leaves(const uint8_t* data, int64_t nbytes, int64_t leaf_bytes
 // reduces [n, 32] digests to one root in place-ish using scratch (same size); returns ptr to root
 int launch_sha256_merkle(uint8_t* level, uint8_t* scratch, int64_t n, uint8_t* root, hipStream_t s);
 
+// ---- gemm.hip ----------------------------------------------------------------------------------
+struct WgradParams {
+  const void* G;   // [M, N] bf16, row stride ldg (grad of the layer output)
+  const void* X;   // [M, K] bf16, row stride ldx (layer input)
+  float* part;     // [S, N, K] fp32 split partials (S > 1)
+  void* out;       // [N, K] bf16, row stride ldo
+  int64_t ldg, ldx, ldo;
+  int M, N, K, S, Mc;
+};
+// number of splits S and rows per split Mc for an M x N x K weight gradient (-1: unsupported)
+int wgrad_splits(int M, int N, int K, int* Mc);
+int launch_wgrad(const WgradParams& p, hipStream_t s);
+
 // ---- attention.hip -----------------------------------------------------------------------------
 struct AttnParams {
   const void* qkv;     // [T, (nh + 2 nkv) * d] bf16

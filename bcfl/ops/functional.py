@@ -22,7 +22,7 @@ from . import rng as _rng
 from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
-           "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear"]
+           "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad"]
 
 
 def _keys(p: float, training: bool):
@@ -31,8 +31,56 @@ def _keys(p: float, training: bool):
     return p8, ka, kb
 
 
+WGRAD_MIN_ROWS = 1024  # below this the weight-gradient GEMM is too small to split profitably
+
+
+def wgrad_supported(g2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Shapes the K9 split-M MFMA weight-gradient kernel takes (bf16, N and K multiples of 128)."""
+    return (g2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and g2.shape[0] >= WGRAD_MIN_ROWS
+            and g2.shape[1] % 128 == 0 and x2.shape[1] % 128 == 0 and g2.stride(1) == 1
+            and x2.stride(1) == 1 and g2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0)
+
+
+def wgrad(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW[N, K] = g2[M, N]^T x2[M, K]: K9 kernel on GPU for supported shapes, library GEMM otherwise."""
+    if use_native(g2) and wgrad_supported(g2, x2):
+        return native().wgrad(g2, x2)
+    return g2.t().mm(x2)
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T (+ b). Forward and input-gradient GEMMs are hipBLASLt (they run at 560-820 TF/s
+    on the BERT shapes); the weight gradient — long reduction over tokens, small output — goes
+    to the split-M MFMA kernel (gemm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        g2 = g.reshape(-1, N)
+        x2 = x.reshape(-1, K)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = g2.mm(w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = wgrad(g2, x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.sum(0)
+        return dx, dw, db
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Plain library GEMM (hipBLASLt via torch) — fused epilogues live in the following op."""
+    """Dense layer. GPU + bf16 + a weight that trains: :class:`_Linear` (library fwd/dgrad GEMMs,
+    hand-written K9 wgrad); otherwise the plain library GEMM."""
+    if (use_native(x) and w.requires_grad and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+            and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0 and x.numel() // w.shape[1] >= WGRAD_MIN_ROWS):
+        return _Linear.apply(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 
 

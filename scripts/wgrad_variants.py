@@ -1,9 +1,11 @@
 """Compare formulations of the weight-gradient GEMM dW[N,K] = G[M,N]^T X[M,K] (M = tokens)."""
 import json
+import os
 import sys
 
 import torch
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from benchmarks.microbench import timeit  # noqa: E402
 
 dev = torch.device("cuda")
