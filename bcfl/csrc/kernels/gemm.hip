@@ -202,8 +202,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 int wgrad_splits(int M, int N, int K, int* Mc) {
   if (N % BT || K % BT || M <= 0) return -1;
   const int tiles = (N / BT) * (K / BT);
-  const int target = 512;  // ~2 resident workgroups per CU on 256 CUs
-  int S = (target + tiles - 1) / tiles;
+  // 2 workgroups fit per CU (64 KiB LDS, 2 waves/SIMD): 512 resident on 256 CUs. Never exceed
+  // one full residency round — a 2nd round of a few workgroups would double the kernel time.
+  const int slots = 512;
+  int S = slots / tiles;
   const int maxS = (M + 255) / 256;  // keep >= 4 pipeline steps per split
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
