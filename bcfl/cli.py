@@ -15,12 +15,36 @@ from typing import List, Optional
 from .config import parse_cli
 
 
+def run_sweep(cfg) -> List[dict]:
+    """Client-count scaling sweep (reference C19: ``for NUM_CLIENTS in [5,10,20]`` wrapping a whole
+    experiment, ``serverless_cancer_biobert_allclients.py:41-46``): one fresh federation per count,
+    each in ``<out_dir>/clients_<n>``, telemetry reset in between. Returns the final records."""
+    import os
+
+    from .fl import Federation
+    out = []
+    for n in cfg.sweep_clients:
+        sub = cfg.replace(num_clients=int(n), sweep_clients=[],
+                          out_dir=os.path.join(cfg.out_dir, f"clients_{int(n)}"))
+        fed = Federation(sub)
+        if fed.verbose:
+            print(f"NUM_CLIENTS = {int(n)}", flush=True)
+        hist = fed.run()
+        out.append({"num_clients": int(n), "rounds": len(hist),
+                    "global_accuracies": list(fed.global_accuracies),
+                    "mean_round_s": sum(h["t_round"] for h in hist) / max(len(hist), 1)})
+    return out
+
+
 def main(argv: Optional[List[str]] = None, default_preset: Optional[str] = None) -> int:
     cfg = parse_cli(argv, default_preset=default_preset)
     from .fl import Federation
     from .parallel import dist as D
-    fed = Federation(cfg)
-    fed.run()
+    if cfg.sweep_clients:
+        run_sweep(cfg)
+    else:
+        fed = Federation(cfg)
+        fed.run()
     D.shutdown()
     return 0
 

@@ -75,6 +75,8 @@ class FLConfig:
     eval_global: bool = True
     metrics_jsonl: bool = True
     reference_prints: bool = True
+    log_provenance: bool = True         # per-round sampled train/test indices (reference C18)
+    sweep_clients: List[int] = field(default_factory=list)  # run once per client count (C19)
     profile: bool = False
     deterministic: bool = False
     seed: int = 42
@@ -163,7 +165,8 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     "serverless_cancer_biobert": dict(mode="serverless", model="biobert", dataset="cancer",
                                       num_labels=41, num_clients=5, num_rounds=20,
                                       partition="iid_random", train_samples=500, test_samples=500,
-                                      resample_each_round=True, compat_save_path="my_albert_model2"),
+                                      resample_each_round=True, compat_save_path="my_albert_model2",
+                                      sweep_clients=[5, 10, 20]),
     # src/Serverlesscase/serverless_caner_classification_iid.py:31-34
     "serverless_cancer_albert_iid": dict(mode="serverless", model="albert-base-v2", dataset="cancer",
                                          num_labels=41, num_clients=10, num_rounds=20,
@@ -228,6 +231,8 @@ def _coerce(field_type: Any, default: Any, raw: str) -> Any:
         return int(raw)
     if isinstance(default, float):
         return float(raw)
+    if isinstance(default, list) and not raw.strip().startswith("["):
+        return [int(x) for x in raw.split(",") if x.strip()]
     if isinstance(default, (dict, list, tuple)):
         if isinstance(default, dict) and ":" in raw and not raw.strip().startswith("{"):
             out = {}

@@ -143,6 +143,7 @@ class Federation:
         self.history: List[dict] = []
         self.start_round = 0
         self.tokens_trained = 0
+        self.provenance_rows = 0
         if cfg.resume:
             self._resume(cfg.resume)
 
@@ -441,7 +442,26 @@ class Federation:
                 "client_metrics": client_metrics, "bytes_sent": 0.0}
 
     # ================================ driver ====================================================
+    def _log_provenance(self, r: int):
+        """Reference C18 (``serverless_IID_IMDB.py:251-260,298-301``): every client's sampled
+        train / test row indices, one JSONL record per (round, client) — written when the draw
+        changes (every round with ``resample_each_round``, else round 0). Partitions are a pure
+        function of the config, so the main rank writes all clients."""
+        if not (self.cfg.log_provenance and self.rt.is_main):
+            return
+        if r != self.start_round and not self.cfg.resample_each_round:
+            return
+        path = os.path.join(self.cfg.out_dir, "provenance.jsonl")
+        os.makedirs(self.cfg.out_dir, exist_ok=True)
+        mode = "a" if (r != self.start_round or self.cfg.resume) else "w"
+        with open(path, mode) as fh:
+            for c, sp in enumerate(self.partitions(r)):
+                fh.write(json.dumps({"round": r, "client": c, "trained_data": [int(i) for i in sp.train],
+                                     "tested_data": [int(i) for i in sp.test]}) + "\n")
+        self.provenance_rows += sum(len(sp.train) for sp in self.partitions(r))
+
     def run_round(self, r: int) -> dict:
+        self._log_provenance(r)
         t0 = time.perf_counter()
         res = self.server_round(r) if self.cfg.mode == "server" else self.serverless_round(r)
         self._maybe_save(r)
@@ -513,6 +533,9 @@ class Federation:
             gdir = os.path.join(self.cfg.out_dir, "global")
             size = dir_size_gb(gdir) if os.path.isdir(gdir) else None
             Telemetry.print_reference_lines(tel, self.global_accuracies, size)
+            if self.cfg.log_provenance:
+                print(f"trained_data / tested_data: {self.provenance_rows} sampled train rows logged to "
+                      f"{os.path.join(self.cfg.out_dir, 'provenance.jsonl')}", flush=True)
         self.metrics.write({"final": True, **tel, "global_accuracies": self.global_accuracies})
         self.metrics.close()
         return tel

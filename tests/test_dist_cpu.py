@@ -106,3 +106,37 @@ def test_serverless_ring_four_ranks(tmp_path):
     res = run_world(_fed_worker, 4, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
     single, _ = _single("serverless", str(tmp_path / "s"), **kw)
     torch.testing.assert_close(res[0]["master"], single, atol=1e-6, rtol=0)
+
+
+def test_round_robin_pairs_cover_every_link():
+    from bcfl.trust.probe import round_robin_pairs
+    for w in (2, 3, 4, 5, 8):
+        rounds = round_robin_pairs(w)
+        seen = [p for r in rounds for p in r]
+        assert len(seen) == len(set(seen)) == w * (w - 1) // 2
+        for r in rounds:  # pairs of one round are disjoint
+            flat = [x for p in r for x in p]
+            assert len(flat) == len(set(flat))
+
+
+def _probe_worker(rank, world):
+    from bcfl.parallel import dist as D
+    from bcfl.trust.probe import measure_bandwidth, probe_and_filter
+    D.init_runtime("cpu", "gloo")
+    bw = measure_bandwidth(nbytes=1 << 18, iters=2)
+    excl = probe_and_filter(torch.zeros(1), num_clients=8, nbytes=1 << 18, iters=2)
+    return {"bw": torch.tensor(bw), "excluded": torch.tensor(excl, dtype=torch.int64)}
+
+
+def test_bandwidth_probe_gloo(tmp_path):
+    res = run_world(_probe_worker, 4, str(tmp_path))
+    bw = res[0]["bw"]
+    assert bw.shape == (4, 4)
+    assert torch.all(torch.diag(bw) == 0)
+    off = bw[~torch.eye(4, dtype=torch.bool)]
+    assert torch.all(off > 0)
+    for r in res[1:]:  # every rank holds the same gathered matrix
+        assert torch.equal(r["bw"], bw)
+    # never a majority excluded; excluded clients come from whole ranks (2 clients per rank)
+    ex = res[0]["excluded"].tolist()
+    assert len(ex) <= 2 and len(ex) % 2 == 0

@@ -142,3 +142,32 @@ def test_llama_lora_federation_delta_only(tmp_out):
     from bcfl.ckpt import read_safetensors
     sd = read_safetensors(os.path.join(tmp_out, "global", "model.safetensors"))
     assert all("lora_" in k or "score" in k for k in sd)
+
+
+def test_provenance_log_records_sampled_indices(tmp_out):
+    cfg = _cfg(tmp_out, mode="serverless", num_rounds=2, ledger=False, save_every=0,
+               partition="iid_random", resample_each_round=True)
+    fed = Federation(cfg, verbose=False)
+    fed.run()
+    recs = [json.loads(x) for x in open(os.path.join(tmp_out, "provenance.jsonl"))]
+    assert sorted({(r["round"], r["client"]) for r in recs}) == [(r, c) for r in range(2) for c in range(3)]
+    for r in recs:
+        sp = fed.partitions(r["round"])[r["client"]]
+        assert r["trained_data"] == [int(i) for i in sp.train]
+        assert r["tested_data"] == [int(i) for i in sp.test]
+        assert len(r["trained_data"]) == 48
+
+
+def test_client_count_sweep_cli(tmp_out):
+    from bcfl.cli import run_sweep
+    from bcfl.config import parse_cli
+    cfg = parse_cli(["--model", "tiny-bert", "--dataset", "tiny", "--num-rounds", "1",
+                     "--train-samples", "32", "--test-samples", "16", "--global-test-samples", "16",
+                     "--batch-size", "16", "--out-dir", tmp_out, "--reference-prints", "false",
+                     "--device", "cpu", "--save-every", "0", "--ledger", "false",
+                     "--sweep-clients", "2,3"])
+    assert cfg.sweep_clients == [2, 3]
+    res = run_sweep(cfg)
+    assert [r["num_clients"] for r in res] == [2, 3]
+    for n in (2, 3):
+        assert os.path.exists(os.path.join(tmp_out, f"clients_{n}", "metrics.jsonl"))
