@@ -64,6 +64,8 @@ class FLConfig:
     # --- fault injection -----------------------------------------------------------
     inject_slow: Dict[int, float] = field(default_factory=dict)       # client -> ms
     inject_byzantine: Dict[int, float] = field(default_factory=dict)  # client -> scale
+    inject_drop: List[int] = field(default_factory=list)  # clients that stop publishing (dead peer)
+    liveness_timeout: int = 2           # rounds without a new version before a peer counts as dead
     # --- io / observability -----------------------------------------------------------
     out_dir: str = "runs/default"
     save_every: int = 1

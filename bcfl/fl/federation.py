@@ -122,7 +122,9 @@ class Federation:
             wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
             if cfg.wire_dtype == "bf16_raw":
                 wire = "bf16"
-            self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip)
+            self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip,
+                                       liveness_timeout=cfg.liveness_timeout)
+            self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
             self.gossip.seed_replicas(self.flat.master)
         # ---------------- trust ---------------------------------------------------------------------
         self.filter = UpdateAnomalyFilter(cfg.anomaly_filter, cfg.anomaly_k,
@@ -397,7 +399,8 @@ class Federation:
         use_v = self.prev_verdicts if cfg.async_gossip else v
         W = mixing_matrix(self.nbrs, cfg.mixing, use_v.rejected)
         with self.timer.phase("comm"):
-            info = self.gossip.end_of_round(r, W, None if self.multi else {self.local_clients[0]: self.flat.param})
+            info = self.gossip.end_of_round(r, W, None if self.multi else {self.local_clients[0]: self.flat.param},
+                                            steps={c: losses[c]["batches"] for c in losses})
         self.prev_verdicts = v
         if self.multi:  # evaluate this rank's first client's mixed model
             self.flat.load_master(self.client_master[self.local_clients[0]])
@@ -413,12 +416,14 @@ class Federation:
                 print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
         train_loss = self._reduce_train_loss(losses)
         self._ledger_round(r, recs, {"kind": "mix", "rejected": sorted(v.rejected),
-                                     "stale_rounds": info.get("stale_rounds", 0.0)})
+                                     "stale_rounds": info.get("stale_rounds", 0.0),
+                                     "dead_peers": sorted(self.gossip.dead)})
         agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
         return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                 "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
-                "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0)}
+                "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
+                "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0)}
 
     def _chain_round(self, r: int) -> dict:
         """Reference C14 exactly: clients train one after another on ONE shared model; the
@@ -476,6 +481,7 @@ class Federation:
                "global_loss": ge.loss if ge is not None else None,
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
+               "dead_peers": res.get("dead_peers", []),
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
         if self.is_cuda:

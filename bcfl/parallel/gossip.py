@@ -17,6 +17,14 @@ What this engine does, per round, for every client ``c`` hosted on this rank:
 3. **mix** — x_c <- W_cc x_c + sum_j W_cj view_j   (one fp32 kernel over the flat buffer), where
    ``view_j`` is the latest *published* state of neighbour j (stale by one round when async).
 
+Message integrity and liveness: every published state carries a
+4-word header ``[version, round, steps, version]`` (seqlock layout — a torn message shows different
+head / tail versions) exchanged in the same grouped batch. A receiver applies a bf16 delta to its
+replica only for ``version == applied + 1`` (a repeated or skipped version never double-applies or
+silently drops an increment), and a neighbour whose version has not advanced for more than
+``liveness_timeout`` rounds is treated as dead: its mixing weight moves to the receiving client's
+self-weight until it publishes again.
+
 Buffers are sized for 288 GB HBM: per remote neighbour one wire buffer + (delta mode) one fp32
 replica — 7 neighbours x (217 MB + 433 MB) ≈ 4.6 GB for BERT-base, ≈ 1.8 GB for Llama-3-8B LoRA.
 """
@@ -35,7 +43,7 @@ from .topology import client_rank
 class GossipEngine:
     def __init__(self, num_clients: int, states: Dict[int, torch.Tensor], nbrs: Dict[int, List[int]],
                  wire: str = "bf16_delta", async_gossip: bool = True, rank: Optional[int] = None,
-                 world: Optional[int] = None):
+                 world: Optional[int] = None, liveness_timeout: int = 2):
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
         self.world = rt.world if world is None else world
@@ -68,6 +76,19 @@ class GossipEngine:
         self.pending: Optional[D.P2PHandle] = None
         self.pending_round: Optional[int] = None
         self.bytes_sent_last = 0
+        # versions / liveness (host bookkeeping + tiny device headers) ---------------------------
+        self.liveness_timeout = liveness_timeout
+        self.version = {c: 0 for c in self.local}            # last published version per local client
+        self.steps = {c: 0 for c in self.local}
+        self.suppressed: set = set()                          # fault injection: clients that stop publishing
+        hz = lambda: torch.zeros(4, dtype=torch.int64, device=self.device)  # noqa: E731
+        self.send_hdr = {c: hz() for c in self.local}
+        self.recv_hdr = {j: hz() for j in self.remote_needed}
+        self.applied = {j: 0 for j in self.remote_needed}     # replica version per remote client
+        self.seen_version = {j: 0 for j in range(self.n)}
+        self.fresh_round = {j: -1 for j in range(self.n)}     # last round j published a new version
+        self.dead: set = set()
+        self.torn = 0
 
     # ------------------------------------------------------------------------------------
     def seed_replicas(self, initial: torch.Tensor):
@@ -88,8 +109,16 @@ class GossipEngine:
         return self.send_buf[j] if local else self.recv_buf[j]
 
     @torch.no_grad()
-    def publish(self):
+    def publish(self, round_idx: int = 0, steps: Optional[Dict[int, int]] = None):
         for c in self.local:
+            if c in self.suppressed:  # simulated dead peer: transport still runs, no new version
+                if self.wire == "bf16_delta":
+                    self.send_buf[c].zero_()
+                continue
+            self.version[c] += 1
+            self.steps[c] += int((steps or {}).get(c, 0))
+            v = self.version[c]
+            self.send_hdr[c].copy_(torch.tensor([v, round_idx, self.steps[c], v], dtype=torch.int64))
             x = self.states[c]
             if self.wire == "bf16_delta":
                 ops.native().delta_encode(x, self.ref[c], self.send_buf[c]) if ops.use_native(x) \
@@ -99,7 +128,9 @@ class GossipEngine:
 
     def launch(self, round_idx: int):
         sends = [(self.send_buf[c], r) for c, r in self.send_plan]
+        sends += [(self.send_hdr[c], r) for c, r in self.send_plan]
         recvs = [(self.recv_buf[j], client_rank(j, self.world)) for j in self.remote_needed]
+        recvs += [(self.recv_hdr[j], client_rank(j, self.world)) for j in self.remote_needed]
         self.bytes_sent_last = sum(t.numel() * t.element_size() for t, _ in sends)
         self.pending = D.p2p_exchange(sends, recvs)
         self.pending_round = round_idx
@@ -110,10 +141,44 @@ class GossipEngine:
             return False
         self.pending.wait()
         self.pending = None
-        if self.wire == "bf16_delta":
-            for j in self.remote_needed:
-                ops.axpby_(self.replica[j], self.recv_buf[j], 1.0, 1.0)
+        rnd = self.pending_round if self.pending_round is not None else 0
+        hdrs = (torch.stack([self.recv_hdr[j] for j in self.remote_needed]).cpu().tolist()
+                if self.remote_needed else [])
+        for j, (v0, _r, _steps, v1) in zip(self.remote_needed, hdrs):
+            if v0 != v1:  # torn message: keep the previous replica
+                self.torn += 1
+                continue
+            if self.wire == "bf16_delta":
+                if v0 == self.applied[j] + 1:
+                    ops.axpby_(self.replica[j], self.recv_buf[j], 1.0, 1.0)
+                    self.applied[j] = v0
+                elif v0 > self.applied[j] + 1:  # a delta was lost: replica can no longer track j
+                    self.dead.add(j)
+            self._note_version(j, v0, rnd)
+        for c in self.local:
+            self._note_version(c, self.version[c], rnd)
         return True
+
+    def _note_version(self, j: int, v: int, rnd: int):
+        if v > self.seen_version[j]:
+            self.seen_version[j] = v
+            self.fresh_round[j] = rnd
+            if self.wire != "bf16_delta" or j in self.states or self.applied.get(j, v) == v:
+                self.dead.discard(j)
+        elif rnd - self.fresh_round[j] > self.liveness_timeout:
+            self.dead.add(j)
+
+    def live_matrix(self, W: np.ndarray) -> np.ndarray:
+        """Mixing matrix with dead neighbours' weights folded into each receiver's self-weight."""
+        if not self.dead:
+            return W
+        W = W.copy()
+        for c in range(self.n):
+            for j in self.dead:
+                if j != c and W[c, j] != 0.0:
+                    W[c, c] += W[c, j]
+                    W[c, j] = 0.0
+        return W
 
     @torch.no_grad()
     def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None):
@@ -125,25 +190,28 @@ class GossipEngine:
 
     # ------------------------------------------------------------------------------------
     def end_of_round(self, round_idx: int, W: np.ndarray,
-                     param_out: Optional[Dict[int, torch.Tensor]] = None) -> Dict[str, float]:
+                     param_out: Optional[Dict[int, torch.Tensor]] = None,
+                     steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
         """Sync: publish -> exchange -> wait -> mix.  Async: wait(prev) -> mix -> publish -> launch."""
         info = {"mixed": 0.0, "stale_rounds": 0.0}
         if not self.async_gossip:
-            self.publish()
+            self.publish(round_idx, steps)
             self.launch(round_idx)
             self.finish()
-            self.mix(W, param_out)
+            self.mix(self.live_matrix(W), param_out)
             info["mixed"] = 1.0
         else:
             had = self.pending is not None
             if had:
                 src_round = self.pending_round
                 self.finish()
-                self.mix(W, param_out)
+                self.mix(self.live_matrix(W), param_out)
                 info.update(mixed=1.0, stale_rounds=float(round_idx - src_round))
-            self.publish()
+            self.publish(round_idx, steps)
             self.launch(round_idx)
         info["bytes_sent"] = float(self.bytes_sent_last)
+        info["dead_peers"] = float(len(self.dead))
+        info["torn"] = float(self.torn)
         return info
 
     def drain(self):

@@ -140,3 +140,42 @@ def test_bandwidth_probe_gloo(tmp_path):
     # never a majority excluded; excluded clients come from whole ranks (2 clients per rank)
     ex = res[0]["excluded"].tolist()
     assert len(ex) <= 2 and len(ex) % 2 == 0
+
+
+def _liveness_worker(rank, world, out):
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.init_runtime("cpu", "gloo")
+    fed = Federation(_cfg("serverless", out, num_rounds=5, inject_drop=[1], liveness_timeout=1,
+                          async_gossip=False, wire_dtype="bf16"), verbose=False)
+    fed.run()
+    return {"dead": torch.tensor(sorted(fed.gossip.dead), dtype=torch.int64),
+            "hist_dead": torch.tensor([len(h["dead_peers"]) for h in fed.history])}
+
+
+def test_gossip_liveness_dead_peer_is_dropped(tmp_path):
+    res = run_world(_liveness_worker, 2, str(tmp_path), str(tmp_path / "o"))
+    # client 1 (rank 1) stops publishing: rank 0 declares it dead once the timeout passes
+    assert res[0]["dead"].tolist() == [1]
+    assert res[0]["hist_dead"][0] == 0 and res[0]["hist_dead"][-1] == 1
+
+
+def _torn_worker(rank, world):
+    from bcfl.parallel import dist as D
+    from bcfl.parallel.gossip import GossipEngine
+    D.init_runtime("cpu", "gloo")
+    x = torch.full((64,), float(rank + 1))
+    eng = GossipEngine(2, {rank: x}, {0: [1], 1: [0]}, "bf16_delta", async_gossip=False)
+    eng.seed_replicas(torch.zeros(64))
+    eng.publish(0)
+    if rank == 1:  # tear the message: head / tail versions differ
+        eng.send_hdr[1][3] += 1
+    eng.launch(0)
+    eng.finish()
+    return {"torn": torch.tensor(eng.torn), "replica": eng.replica[1 - rank].clone()}
+
+
+def test_gossip_torn_message_not_applied(tmp_path):
+    res = run_world(_torn_worker, 2, str(tmp_path))
+    assert int(res[0]["torn"]) == 1 and torch.all(res[0]["replica"] == 0)  # rank 1's message rejected
+    assert int(res[1]["torn"]) == 0 and torch.all(res[1]["replica"] == 1.0)
