@@ -185,6 +185,15 @@ PRESETS: Dict[str, Dict[str, Any]] = {
                                                num_labels=41, num_clients=2, num_rounds=2,
                                                partition="iid_random", train_samples=500,
                                                test_samples=500, resample_each_round=True),
+    # real-text variants of the medical scripts on the reference's local CSVs (C6) ---------
+    "serverless_NonIID_medical_csv": dict(mode="serverless", model="biobert", dataset="medical_csv",
+                                          num_labels=40, num_clients=10, num_rounds=20,
+                                          partition="ref_contiguous", train_samples=400,
+                                          test_samples=400, max_seq_len=128),
+    "server_iid_medical_csv": dict(mode="server", model="biobert", dataset="medical_csv",
+                                   num_labels=40, num_clients=5, num_rounds=20,
+                                   partition="iid_random", train_samples=500, test_samples=500,
+                                   max_seq_len=128),
     # BASELINE.json configs --------------------------------------------------------------
     "baseline1_distilbert_server_iid_cpu": dict(mode="server", model="distilbert", dataset="imdb",
                                                 num_labels=2, num_clients=2, num_rounds=2,

@@ -43,7 +43,15 @@ DATASETS: Dict[str, DatasetSpec] = {
                          "synthetic covid_final-shaped sentiment (3 classes)"),
     # tiny split for unit tests
     "tiny": DatasetSpec("tiny", 2, 512, 256, 24.0, 0.4, 40, 32, True, "tiny test split"),
+    # REAL text from the reference's local CSVs, WordPiece trained offline
+    # (bcfl.data.text); shard strides follow the medical scripts (Serverless_NonIID_Medical:55-56)
+    "medical_csv": DatasetSpec("medical_csv", 40, 12000, 3000, 28.0, 0.45, 500, 400, False,
+                               "Medical Transcriptions CSV (reference Dataset/*_mt.csv), real text"),
+    "selfdriving_csv": DatasetSpec("selfdriving_csv", 3, 400, 100, 12.0, 0.3, 40, 32, False,
+                                   "self-driving sentiment CSV (reference Dataset/), real text"),
 }
+
+TEXT_DATASETS = ("medical_csv", "selfdriving_csv")
 
 
 def get_dataset(name: str) -> DatasetSpec:
@@ -56,6 +64,9 @@ def get_dataset(name: str) -> DatasetSpec:
 def load_split(name: str, split: str, vocab_size: int, max_len: int = 512, seed: int = 1234,
                cls_id: int = 101, sep_id: int = 102) -> TokenDataset:
     spec = get_dataset(name)
+    if name in TEXT_DATASETS:
+        from .text import load_csv_split
+        return load_csv_split(name, split, vocab_size, max_len, cls_id, sep_id)
     n = spec.n_train if split == "train" else spec.n_test
     split_seed = seed * 7919 + (0 if split == "train" else 1)
     return make_synthetic_split(n, spec.num_classes, vocab_size, seed=split_seed,
