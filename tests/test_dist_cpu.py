@@ -179,3 +179,17 @@ def test_gossip_torn_message_not_applied(tmp_path):
     res = run_world(_torn_worker, 2, str(tmp_path))
     assert int(res[0]["torn"]) == 1 and torch.all(res[0]["replica"] == 0)  # rank 1's message rejected
     assert int(res[1]["torn"]) == 0 and torch.all(res[1]["replica"] == 1.0)
+
+
+def test_info_passing_benchmark_gloo(tmp_path):
+    import json as _json
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from benchmarks.info_passing import _cpu_worker
+    out = str(tmp_path / "r.json")
+    run_world(_cpu_worker, 3, str(tmp_path), 50_000, out)
+    res = _json.load(open(out))
+    assert res["world"] == 3 and len(res["sources"]) == 3
+    for s in res["sources"]:
+        assert s["measured_sync_s"] > 0 and s["measured_async_s"] > 0
+        assert s["predicted_async_s"] <= s["predicted_sync_s"]

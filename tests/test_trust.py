@@ -124,3 +124,34 @@ def test_ledger_chain(native, tmp_path):
     assert other.tip == L2.tip
     blk = L2.block(3)
     assert block_hash(blk) == blk["hash"]
+
+
+def test_report_cli_reproduces_notebook_outputs(tmp_path):
+    from bcfl.trust.report import analyse, main
+    rep = analyse(__import__("bcfl.trust.netdata", fromlist=["x"]).REF_BW_MBPS)
+    assert rep["anomalies"]["pagerank"] == [0, 4, 7, 9]
+    assert rep["anomalies"]["modz"] == [8, 9]
+    assert rep["anomalies"]["dbscan"] == [] and rep["anomalies"]["louvain"] == []
+    lo, hi = rep["pagerank_thresholds"]
+    assert abs(lo - 0.08349251192983634) < 1e-9 and abs(hi - 0.11650748807016365) < 1e-9
+    for r in rep["info_passing"]:
+        assert r["async_s"] <= r["sync_s"] and r["async_filtered_s"] <= r["sync_filtered_s"] + 1e-12
+    out = tmp_path / "rep.json"
+    assert main(["--json", str(out)]) == 0 and out.exists()
+
+
+def test_plots_from_metrics(tmp_path):
+    pytest.importorskip("matplotlib")
+    import json as _json
+    from bcfl.trust.report import analyse
+    from bcfl.trust.netdata import REF_BW_MBPS
+    from bcfl.utils import plots
+    m = tmp_path / "metrics.jsonl"
+    with open(m, "w") as fh:
+        for r in range(3):
+            fh.write(_json.dumps({"round": r, "t_round": 0.5 + r, "global_acc": 0.5 + 0.1 * r}) + "\n")
+    rep = tmp_path / "rep.json"
+    rep.write_text(_json.dumps(analyse(REF_BW_MBPS)))
+    assert plots.main(["--metrics", str(m), "--report", str(rep), "--out", str(tmp_path / "figs")]) == 0
+    for f in ("global_accuracy.png", "round_time.png", "info_passing.png"):
+        assert (tmp_path / "figs" / f).stat().st_size > 1000
