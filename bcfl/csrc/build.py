@@ -68,6 +68,15 @@ def _torch_flags():
     return incs, libs, abi
 
 
+# Per-file code-generation flags. ``-amdgpu-mfma-vgpr-form``: MFMA results land in ordinary VGPRs
+# instead of AGPRs — the attention kernels post-process every score tile with VALU ops, so AGPR
+# accumulators cost one v_accvgpr_read per element per tile; without them the flash-attention
+# kernels need no AGPRs at all and reach 3 waves/SIMD instead of 2.
+FILE_FLAGS = {
+    "attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+}
+
+
 def build_kernels(force=False, verbose=False, jobs=8) -> str:
     kern = sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(HERE, "kernels", "*.h")))
@@ -84,7 +93,8 @@ def build_kernels(force=False, verbose=False, jobs=8) -> str:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _stale(o, [s, *hdrs, __file__]):
-            jobs_list.append([HIPCC, *common, "-ffp-contract=fast", "-munsafe-fp-atomics", "-c", s, "-o", o])
+            jobs_list.append([HIPCC, *common, "-ffp-contract=fast", "-munsafe-fp-atomics",
+                              *FILE_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o])
     tinc = sum((["-isystem", p] for p in incs + _py_includes()), [])
     bo = os.path.join(BUILD, "bindings.o")
     objs.append(bo)
