@@ -205,34 +205,48 @@ std::vector<Tensor> emb_ln_fwd(Tensor ids, Tensor pos, optional<Tensor> tt, Tens
   return {out, z, mean, rstd};
 }
 
+// Embedding + LN backward without atomics: the LN backward (dropout on the output side) writes
+// dx [T, H]; the word / position / type table gradients are deterministic segmented row sums over
+// the stably sorted ids (one wave per run of equal ids), written straight into zeroed tables of
+// the parameter dtype — no fp32 [V, H] buffer, no atomics, no cast pass.
 std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Tensor> tt, Tensor z,
                                Tensor mean, Tensor rstd, Tensor gamma, int64_t V, int64_t P,
                                int64_t TV, int64_t p8, int64_t ka, int64_t kb) {
   check_cuda(dout, "dout");
   const int T = ids.numel(), H = z.size(1);
-  auto f = z.options().dtype(torch::kFloat);
-  auto dword = torch::zeros({V, H}, f);
-  Tensor dpos = P > 0 ? torch::zeros({P, H}, f) : Tensor();
-  Tensor dtype_ = TV > 0 ? torch::zeros({TV, H}, f) : Tensor();
+  const int dt = dt_of(z);
+  auto popt = z.options();
+  auto f = popt.dtype(torch::kFloat);
+  const int* ttp = tt.has_value() && tt->defined() ? tt->data_ptr<int>() : nullptr;
+  const bool tsum = TV > 0 && ttp == nullptr;  // implicit type id 0: row 0 gets the column sum
+  auto dx = torch::empty_like(z);
   const int nblk = bcfl::bwd_blocks(T);
   auto partial = torch::empty({nblk, 3, H}, f);
-  const int* ttp = tt.has_value() && tt->defined() ? tt->data_ptr<int>() : nullptr;
-  const int dt = dt_of(z);
-  check_rc(bcfl::launch_emb_ln_bwd(dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(),
-                                   rstd.data_ptr<float>(), gamma.data_ptr(), ids.data_ptr<int>(),
-                                   pos.data_ptr<int>(), ttp, dword.data_ptr<float>(),
-                                   P > 0 ? dpos.data_ptr<float>() : nullptr,
-                                   TV > 0 ? dtype_.data_ptr<float>() : nullptr,
-                                   partial.data_ptr<float>(), nblk, T, H, (uint32_t)p8,
-                                   (uint32_t)ka, (uint32_t)kb, dt, stream()),
+  check_rc(bcfl::launch_bdaln_bwd(dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(),
+                                  rstd.data_ptr<float>(), gamma.data_ptr(), dx.data_ptr(), nullptr,
+                                  partial.data_ptr<float>(), nblk, T, H, (uint32_t)p8, (uint32_t)ka,
+                                  (uint32_t)kb, tsum ? 1 : 0, dt, stream(), /*drop_in=*/1),
            "emb_ln_bwd");
-  auto popt = z.options();
+  auto piece = torch::empty({T, H}, f);
+  auto table_grad = [&](const Tensor& key32, int64_t rows) {
+    auto g = torch::zeros({rows, H}, popt);
+    auto sorted = at::sort(key32.to(torch::kLong), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    const Tensor& sk = std::get<0>(sorted);
+    const Tensor& perm = std::get<1>(sorted);
+    check_rc(bcfl::launch_segment_rowsum(dx.data_ptr(), dt, sk.data_ptr<int64_t>(),
+                                         perm.data_ptr<int64_t>(), piece.data_ptr<float>(),
+                                         g.data_ptr(), dt, T, H, stream()),
+             "segment_rowsum");
+    return g;
+  };
+  Tensor dword = table_grad(ids, V);
+  Tensor dpos = P > 0 ? table_grad(pos, P) : Tensor();
+  Tensor dtype_;
+  if (TV > 0) dtype_ = ttp ? table_grad(*tt, TV) : torch::zeros({TV, H}, popt);
   auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);
-  // plane 2: implicit type id 0 -> row 0 of the type table gets the column sum of dz
-  const bool tsum = TV > 0 && ttp == nullptr;
   check_rc(bcfl::launch_colsum3(partial.data_ptr<float>(), nblk, H, dgamma.data_ptr(),
-                                dbeta.data_ptr(), tsum ? dtype_.data_ptr() : nullptr, dt, dt,
-                                bcfl::DT_F32, stream()), "colsum3");
+                                dbeta.data_ptr(), tsum ? dtype_.data_ptr() : nullptr, dt, dt, dt,
+                                stream()), "colsum3");
   return {dword, dpos, dtype_, dgamma, dbeta};
 }
 

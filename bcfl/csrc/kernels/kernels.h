@@ -16,7 +16,12 @@ int launch_bdaln_fwd(const void* y, const void* bias, const void* res, const voi
                      float eps, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
 int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
                      const void* gamma, void* dz, void* dy, float* partial, int nblk, int T, int H,
-                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s);
+                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s,
+                     int drop_in = 0);
+// dst[keys[i]] = sum of src[perm[j]] over the run of equal sorted keys starting at i (no atomics,
+// deterministic); piece: fp32 [T, H] scratch
+int launch_segment_rowsum(const void* src, int src_dt, const int64_t* keys, const int64_t* perm,
+                          float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s);
 int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,
                   hipStream_t s);
 // reduce planes 0..2 of partial[nblk][3][H] into out0..2 (nullptr = skip) in one launch

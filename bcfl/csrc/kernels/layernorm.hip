@@ -87,13 +87,18 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_fwd_kernel(
   if (lane == 0 && mean_out) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
-// partial[block][k][H], k = 0: dgamma, 1: dbeta, 2: dbias
+// partial[block][k][H], k = 0: dgamma, 1: dbeta, 2: dbias (= column sum of dy)
+// drop_in = 0: dropout sits BEFORE the LN (bias-dropout-add-LN): dy = keep(dz) / (1-p).
+// drop_in = 1: dropout sits AFTER the LN (embedding LN): dout is masked first, dy = dz.
+// The next row's dout / z / stats are loaded into registers before the current row's reductions
+// (two rows in flight per wave: one memory round-trip hidden behind each row's math), and the
+// dropout hash is evaluated once per 4 consecutive elements (bcfl/ops/rng.py keep layout).
 template <typename TA, typename TP, int NCH>
 __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
     const TA* __restrict__ dout, const TA* __restrict__ z, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const TP* __restrict__ gamma, TA* __restrict__ dz_out,
     TA* __restrict__ dy_out, float* __restrict__ partial, int T, int H, uint32_t p8, uint32_t ka,
-    uint32_t kb, int want_dbias) {
+    uint32_t kb, int want_dbias, int drop_in) {
   __shared__ float red[LN_WAVES][3][NCH * 4 * WAVE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float sc = p8 ? keep_scale(p8) : 1.f;
@@ -111,26 +116,52 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
       else { gm[i][0] = gm[i][1] = gm[i][2] = gm[i][3] = 1.f; }
     }
   }
-  for (int row = blockIdx.x * LN_WAVES + wid; row < T; row += gridDim.x * LN_WAVES) {
+  const int stride = gridDim.x * LN_WAVES;
+  int row = blockIdx.x * LN_WAVES + wid;
+  float nd[NCH][4], nz[NCH][4], nmean = 0.f, nrstd = 0.f;
+  auto fetch = [&](int r) {
+    if (r < T) {
+      const size_t bs = (size_t)r * H;
+      nmean = mean_in[r];
+      nrstd = rstd_in[r];
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int col = (lane + i * WAVE) * 4;
+        if (col < H) {
+          Vec4<TA>::load(dout + bs + col, nd[i]);
+          Vec4<TA>::load(z + bs + col, nz[i]);
+        }
+      }
+    }
+  };
+  fetch(row);
+  for (; row < T; row += stride) {
     const size_t base = (size_t)row * H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NCH][4], g[NCH][4];
+    const float mean = nmean, rstd = nrstd;
+    float d[NCH][4], xh[NCH][4], g[NCH][4];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { d[i][k] = nd[i][k]; xh[i][k] = nz[i][k]; }
+    fetch(row + stride);  // in flight during this row's math
+    uint32_t hs[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      hs[i] = p8 ? hash32((uint32_t)(base + (lane + i * WAVE) * 4) >> 2, ka, kb) : 0u;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int col = (lane + i * WAVE) * 4;
       if (col < H) {
-        float d[4], zz[4];
-        Vec4<TA>::load(dout + base + col, d);
-        Vec4<TA>::load(z + base + col, zz);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          xh[i][k] = (zz[k] - mean) * rstd;
-          g[i][k] = d[k] * gm[i][k];
+          if (p8 && drop_in) d[i][k] = (((hs[i] >> (8 * k)) & 0xffu) >= p8) ? d[i][k] * sc : 0.f;
+          xh[i][k] = (xh[i][k] - mean) * rstd;
+          g[i][k] = d[i][k] * gm[i][k];
           s1 += g[i][k];
           s2 += g[i][k] * xh[i][k];
-          dg[i][k] += d[k] * xh[i][k];
-          db[i][k] += d[k];
+          dg[i][k] += d[i][k] * xh[i][k];
+          db[i][k] += d[i][k];
         }
       }
     }
@@ -144,7 +175,7 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           dz[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
-          dy[k] = p8 ? (keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? dz[k] * sc : 0.f) : dz[k];
+          dy[k] = (p8 && !drop_in) ? ((((hs[i] >> (8 * k)) & 0xffu) >= p8) ? dz[k] * sc : 0.f) : dz[k];
           dbi[i][k] += dy[k];
         }
         Vec4<TA>::store(dz_out + base + col, dz);
@@ -171,6 +202,128 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
       for (int w = 0; w < LN_WAVES; ++w) a += red[w][k][j];
       partial[((size_t)blockIdx.x * 3 + k) * H + j] = a;
     }
+  }
+}
+
+// Deterministic segmented row sum (embedding-table gradients without atomics). keys[] sorted
+// ascending (stable), perm[i] = source row of sorted position i (both < 2^31). Token frequencies
+// are Zipf-like — one run of equal keys can hold thousands of rows — so the sum is split in two
+// passes and neither walks a long run with dependent memory round trips:
+//   pass 1: one wave per chunk of SEG_C sorted positions. The chunk's keys / source rows are read
+//           once into lanes (v_readlane afterwards, no memory latency in the control flow), all
+//           SEG_C source rows are loaded up front (SEG_C x NCH independent 8/16-byte loads in
+//           flight), then every run-PIECE of the chunk is summed in fp32 and written at the
+//           piece's first position of `piece` [T, H];
+//   pass 2: one wave per run head finds how many following chunks the run continues into with
+//           one lane-parallel key probe + ballot per 64 chunks, then adds the piece sums (at the
+//           head and at each continued chunk's first position) in position order -> dst[key].
+// Fixed summation order throughout, so the result is bitwise reproducible.
+constexpr int SEG_C = 16;
+
+template <typename TA, int NCH>
+__global__ __launch_bounds__(256) void segment_pass1_kernel(const TA* __restrict__ src,
+                                                            const int64_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ perm,
+                                                            float* __restrict__ piece, int T, int H) {
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int p0 = chunk * SEG_C;
+  if (p0 >= T) return;
+  const int n = min(SEG_C, T - p0);
+  const int kl = lane < n ? (int)keys[p0 + lane] : -1;
+  const int pl = lane < n ? (int)perm[p0 + lane] : 0;
+  // rows are loaded R at a time (R x NCH independent loads in flight, bounded registers)
+  constexpr int R = NCH <= 1 ? 16 : (NCH <= 3 ? 8 : (NCH <= 6 ? 4 : 2));
+  float a[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[i][k] = 0.f;
+  int head = 0, key = __builtin_amdgcn_readlane(kl, 0);
+  auto flush = [&](int h) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      if (col < H) Vec4<float>::store(piece + (size_t)(p0 + h) * H + col, a[i]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[i][k] = 0.f;
+    }
+  };
+#pragma unroll
+  for (int r0 = 0; r0 < SEG_C; r0 += R) {
+    if (r0 < n) {
+      float v[R][NCH][4];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r0 + r < n) {
+          const size_t row = (size_t)__builtin_amdgcn_readlane(pl, r0 + r) * H;
+#pragma unroll
+          for (int i = 0; i < NCH; ++i) {
+            const int col = (lane + i * WAVE) * 4;
+            if (col < H) Vec4<TA>::load(src + row + col, v[r][i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r0 + r < n) {
+          const int kr = __builtin_amdgcn_readlane(kl, r0 + r);
+          if (kr != key) {
+            flush(head);
+            head = r0 + r;
+            key = kr;
+          }
+#pragma unroll
+          for (int i = 0; i < NCH; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) a[i][k] += v[r][i][k];
+        }
+      }
+    }
+  }
+  flush(head);
+}
+
+template <typename TD>
+__global__ __launch_bounds__(256) void segment_pass2_kernel(const float* __restrict__ piece,
+                                                            const int64_t* __restrict__ keys,
+                                                            TD* __restrict__ dst, int T, int H) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= T) return;
+  const int64_t key = keys[i];
+  if (i > 0 && keys[i - 1] == key) return;  // not a run head (wave-uniform)
+  // continuation chunks: first positions c1, c1 + SEG_C, ... whose key still equals `key`
+  const int c1 = (i / SEG_C + 1) * SEG_C;
+  int m = 0;  // number of continued chunks
+  for (;;) {
+    const int pos = c1 + (m + lane) * SEG_C;
+    const bool differs = pos >= T || keys[pos] != key;
+    const uint64_t bal = __ballot(differs);
+    if (bal) {
+      m += __builtin_ctzll(bal);
+      break;
+    }
+    m += WAVE;
+  }
+  for (int c0 = lane * 4; c0 < H; c0 += WAVE * 4) {
+    float a[4];
+    Vec4<float>::load(piece + (size_t)i * H + c0, a);
+    int b = 0;
+    for (; b + 4 <= m; b += 4) {  // 4 independent loads in flight
+      float q[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Vec4<float>::load(piece + (size_t)(c1 + (b + u) * SEG_C) * H + c0, q[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += q[u][k];
+    }
+    for (; b < m; ++b) {
+      float q[4];
+      Vec4<float>::load(piece + (size_t)(c1 + b * SEG_C) * H + c0, q);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += q[k];
+    }
+    Vec4<TD>::store(dst + (size_t)key * H + c0, a);
   }
 }
 
@@ -786,11 +939,12 @@ int launch_bdaln_fwd(const void* y, const void* bias, const void* res, const voi
 
 int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
                      const void* gamma, void* dz, void* dy, float* partial, int nblk, int T, int H,
-                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s) {
+                     uint32_t p8, uint32_t ka, uint32_t kb, int want_dbias, int dt, hipStream_t s,
+                     int drop_in) {
   if (H % 4) return -2;
   // measured on MI355X (BERT-base, T~8.3k): the wave-per-row kernel below is 1.8x faster than the
   // half-wave variant (whose 3-plane LDS combine dominates); keep the latter for reference.
-  if (use8(H) && false) {
+  if (use8(H) && false && !drop_in) {
     const size_t lds = (size_t)HR * H * sizeof(float);
     DT_DISPATCH(dt, NC8_DISPATCH(H, hipLaunchKernelGGL((bdaln8_bwd_kernel<TA, TP, NC>), dim3(nblk),
         dim3(LN_THREADS), lds, s, (const TA*)dout, (const TA*)z, mean, rstd, (const TP*)gamma,
@@ -799,7 +953,28 @@ int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const f
   }
   DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((bdaln_bwd_kernel<TA, TP, NC>), dim3(nblk),
       dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)z, mean, rstd, (const TP*)gamma,
-      (TA*)dz, (TA*)dy, partial, T, H, p8, ka, kb, want_dbias)));
+      (TA*)dz, (TA*)dy, partial, T, H, p8, ka, kb, want_dbias, drop_in)));
+  return 0;
+}
+
+int launch_segment_rowsum(const void* src, int src_dt, const int64_t* keys, const int64_t* perm,
+                          float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (H % 4) return -2;
+  dim3 g1(((T + SEG_C - 1) / SEG_C + 3) / 4), g2((T + 3) / 4);
+  if (src_dt == DT_BF16) {
+    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<bf16_t, NC>), g1, dim3(256), 0, s,
+                                             (const bf16_t*)src, keys, perm, piece, T, H));
+  } else {
+    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<float, NC>), g1, dim3(256), 0, s,
+                                             (const float*)src, keys, perm, piece, T, H));
+  }
+  if (dst_dt == DT_BF16)
+    hipLaunchKernelGGL((segment_pass2_kernel<bf16_t>), g2, dim3(256), 0, s, piece, keys,
+                       (bf16_t*)dst, T, H);
+  else
+    hipLaunchKernelGGL((segment_pass2_kernel<float>), g2, dim3(256), 0, s, piece, keys, (float*)dst,
+                       T, H);
   return 0;
 }
 

@@ -121,11 +121,15 @@ def test_attention_lse():
     _close(lse, rl, 1e-2, 1e-3)
 
 
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_embedding_layernorm(p):
+@pytest.mark.parametrize("p,skew", [(0.0, False), (0.1, False), (0.1, True)])
+def test_embedding_layernorm(p, skew):
     torch.manual_seed(0)
-    V, P, H, T = 1000, 128, 768, 300
+    V, P, H, T = 1000, 128, 768, 3000 if skew else 300
     ids = torch.randint(0, V, (T,), device=DEV, dtype=torch.int32)
+    if skew:  # Zipf-like: runs far longer than the 32-row segment chunk, plus many singletons
+        ids[: T // 2] = 7
+        ids[T // 2: T // 2 + 300] = 3
+    pos = torch.randint(0, P, (T,), device=DEV, dtype=torch.int32)
     pos = torch.randint(0, P, (T,), device=DEV, dtype=torch.int32)
     ws = [(0.02 * torch.randn(*s, device=DEV)).bfloat16().requires_grad_(True) for s in ((V, H), (P, H), (2, H))]
     g = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
@@ -141,6 +145,15 @@ def test_embedding_layernorm(p):
     out.backward(go)
     r.backward(go.float())
     _grads_close([w.grad for w in ws] + [g.grad, be.grad], [l.grad for l in leaves])
+    if skew:  # the long runs themselves, and bitwise determinism of the segmented sums
+        # row 7 sums 1500 token rows (|grad| ~ 1e3, bf16 ulp ~ 8): compare by relative norm
+        _grads_close([ws[0].grad[7], ws[0].grad[3]], [leaves[0].grad[7], leaves[0].grad[3]], 1e-2)
+        g1 = ws[0].grad.clone()
+        for w in ws:
+            w.grad = None
+        rng.manual_seed(11)
+        ops.embedding_layernorm(ids, pos, None, *ws, g, be, 1e-12, p, True).backward(go)
+        assert torch.equal(ws[0].grad, g1)
 
 
 def test_rmsnorm_rope_swiglu():
