@@ -104,7 +104,7 @@ def main():
             "accuracy_note": "synthetic IMDB-shaped data + random-init weights; not comparable to pretrained accuracy on real IMDB",
             "tokens_per_s": tokens / dt,
             "samples_per_s": a.clients * cfg.train_samples * a.steps / dt,
-            "dtype": "bf16",
+            "dtype": "bf16" if fed.dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (IMDB-shaped lengths, label-sorted Non-IID shards, packed varlen); random-init weights",
             "config": {"model": a.model, "global_batch": 32 * a.clients, "seq_len": 512,
                        "parallelism": f"fl{a.clients}-clients-on-{rt.world}gpu",
