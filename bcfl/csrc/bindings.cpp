@@ -441,7 +441,7 @@ Tensor sha256_merkle(Tensor leaves) {
 
 // ------------------------------------------------------------------------------------------------
 // dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
-Tensor wgrad(Tensor g, Tensor x) {
+std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   TORCH_CHECK(g.is_cuda() && x.is_cuda(), "wgrad: GPU tensors required");
   TORCH_CHECK(g.dim() == 2 && x.dim() == 2 && g.size(0) == x.size(0), "wgrad: g [M,N], x [M,K]");
   TORCH_CHECK(g.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16");
@@ -456,9 +456,22 @@ Tensor wgrad(Tensor g, Tensor x) {
   if (S > 1) part = torch::empty({S, N, K}, g.options().dtype(torch::kFloat));
   bcfl::WgradParams p{g.data_ptr(), x.data_ptr(), S > 1 ? part.data_ptr<float>() : nullptr,
                       out.data_ptr(), g.stride(0), x.stride(0), K, M, N, K, S, Mc};
+  Tensor db, dbp;
+  if (with_bias) {
+    db = torch::empty({N}, g.options());
+    dbp = torch::empty({S, N}, g.options().dtype(torch::kFloat));
+    p.dbias_part = dbp.data_ptr<float>();
+    p.dbias = db.data_ptr();
+  }
   check_rc(bcfl::launch_wgrad(p, stream()), "wgrad");
-  return out;
+  if (with_bias) return {out, db};
+  return {out};
 }
+
+Tensor wgrad(Tensor g, Tensor x) { return wgrad_impl(g, x, false)[0]; }
+
+// (dW, db) with db = colsum(g) fused into the weight-gradient kernel
+std::vector<Tensor> wgrad_bias(Tensor g, Tensor x) { return wgrad_impl(g, x, true); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "bcfl gfx950 (CDNA4) kernels";
@@ -467,6 +480,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("wgrad", &wgrad);
+  m.def("wgrad_bias", &wgrad_bias);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);

@@ -12,6 +12,8 @@
 //     ds_read_b64_tr_b16 hardware-transposed reads — no transpose pass over G or X;
 //   * global loads of step i+2 are in flight (two register sets) during the MFMAs of steps i and
 //     i+1, one barrier per step (double-buffered LDS);
+//   * optionally the bias gradient db = colsum(G) is fused in (the G fragments are already in
+//     registers), replacing a separate full read of G;
 //   * the workgroup -> (split, tile) map is XCD-aware: the 8 XCDs each own a contiguous range of
 //     logical ids, so concurrently running tiles of one XCD share the same G/X rows in its L2.
 //
@@ -91,6 +93,10 @@ __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+  // fused bias gradient db[n] = sum_m G[m, n]: the waves of the k0 == 0 tiles with wk == 0 add up
+  // the G fragments they already hold (lane: column n, 8 of the 16 rows of each k-step)
+  const bool do_bias = p.dbias_part != nullptr && k0 == 0 && wk == 0;
+  float cs[2] = {0.f, 0.f};
 
   if (nsteps > 0) {  // workgroup-uniform
     // transposed-read lane offsets of this wave's two G column blocks (u = 2wn + i) and two X
@@ -147,6 +153,12 @@ __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], bx[j], acc[i][j]);
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[i] += (float)a[i][e];
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       bf16_t* nx = lds + ((it + 1) & 1) * STG;
@@ -160,6 +172,19 @@ __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
     }
   }
 
+  if (do_bias) {  // lanes l and l + 32 hold the two k-halves of column n
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float t = cs[i] + __shfl_xor(cs[i], 32, 64);
+      const int n = n0 + 64 * wn + 32 * i + (lane & 31);
+      if (hh == 0) {
+        if (p.S == 1)
+          reinterpret_cast<bf16_t*>(p.dbias)[n] = f2bf(t);
+        else
+          p.dbias_part[(int64_t)s * p.N + n] = t;
+      }
+    }
+  }
   // epilogue: accumulator column = lane & 31 -> k, rows acc_row -> n
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -197,6 +222,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   Vec4<bf16_t>::store(out + n * ldo + k, v);
 }
 
+// db[n] = bf16( sum_s part[s, n] )
+__global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* __restrict__ part, int S,
+                                                                int N, bf16_t* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += part[(int64_t)s * N + n];
+  out[n] = f2bf(a);
+}
+
 }  // namespace
 
 int wgrad_splits(int M, int N, int K, int* Mc) {
@@ -224,6 +259,9 @@ int launch_wgrad(const WgradParams& p, hipStream_t s) {
     const int64_t n4 = (int64_t)p.N * p.K / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
                        p.part, p.S, p.N, p.K, reinterpret_cast<bf16_t*>(p.out), p.ldo);
+    if (p.dbias_part)
+      hipLaunchKernelGGL(wgrad_bias_reduce_kernel, dim3((p.N + 255) / 256), dim3(256), 0, s,
+                         p.dbias_part, p.S, p.N, reinterpret_cast<bf16_t*>(p.dbias));
   }
   return 0;
 }

@@ -81,6 +81,8 @@ struct WgradParams {
   void* out;       // [N, K] bf16, row stride ldo
   int64_t ldg, ldx, ldo;
   int M, N, K, S, Mc;
+  float* dbias_part = nullptr;  // [S, N] fp32 partial bias gradients (nullptr: no bias)
+  void* dbias = nullptr;        // [N] bf16 bias gradient
 };
 // number of splits S and rows per split Mc for an M x N x K weight gradient (-1: unsupported)
 int wgrad_splits(int M, int N, int K, int* Mc);

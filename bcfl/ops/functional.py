@@ -68,9 +68,13 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = g2.mm(w).view(x.shape)
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            dw = wgrad(g2, x2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if want_b and use_native(g2) and wgrad_supported(g2, x2):
+                dw, db = native().wgrad_bias(g2, x2)  # bias gradient fused into the K9 kernel
+            else:
+                dw = wgrad(g2, x2)
+        if want_b and db is None:
             db = g2.sum(0)
         return dx, dw, db
 

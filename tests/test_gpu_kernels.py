@@ -321,6 +321,10 @@ def test_wgrad_split_m(M, N, K):
     assert err < 5e-3, err
     out2 = ops.native().wgrad(g, x)
     assert torch.equal(out, out2)  # deterministic split reduction
+    ow, db = ops.native().wgrad_bias(g, x)  # fused bias gradient = column sums of g
+    assert torch.equal(ow, out)
+    rb = g.float().sum(0)
+    assert ((db.float() - rb).norm() / rb.norm()) < 5e-3
 
 
 def test_linear_autograd_uses_wgrad_kernel():
