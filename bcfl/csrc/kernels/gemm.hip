@@ -66,6 +66,7 @@ struct StageTile {
   }
 };
 
+template <bool BIAS>
 __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);  // [2 stages][G tile | X tile]
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
   // fused bias gradient db[n] = sum_m G[m, n]: the waves of the k0 == 0 tiles with wk == 0 add up
   // the G fragments they already hold (lane: column n, 8 of the 16 rows of each k-step)
-  const bool do_bias = p.dbias_part != nullptr && k0 == 0 && wk == 0;
+  const bool do_bias = BIAS && k0 == 0 && wk == 0;  // BIAS: compile-time, no cost otherwise
   float cs[2] = {0.f, 0.f};
 
   if (nsteps > 0) {  // workgroup-uniform
@@ -254,7 +255,10 @@ int launch_wgrad(const WgradParams& p, hipStream_t s) {
   if (p.N % BT || p.K % BT || p.S < 1 || (p.S > 1 && !p.part)) return -1;
   const int tiles = (p.N / BT) * (p.K / BT);
   const size_t lds = (size_t)2 * 2 * BM * BT * sizeof(bf16_t);
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * p.S), dim3(TPB), lds, s, p);
+  if (p.dbias_part)
+    hipLaunchKernelGGL(wgrad_kernel<true>, dim3(tiles * p.S), dim3(TPB), lds, s, p);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<false>, dim3(tiles * p.S), dim3(TPB), lds, s, p);
   if (p.S > 1) {
     const int64_t n4 = (int64_t)p.N * p.K / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,

@@ -79,11 +79,15 @@ class _Linear(torch.autograd.Function):
         return dx, dw, db
 
 
+def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (use_native(x) and w.requires_grad and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+            and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0 and x.numel() // w.shape[1] >= WGRAD_MIN_ROWS)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Dense layer. GPU + bf16 + a weight that trains: :class:`_Linear` (library fwd/dgrad GEMMs,
     hand-written K9 wgrad); otherwise the plain library GEMM."""
-    if (use_native(x) and w.requires_grad and torch.is_grad_enabled() and x.dtype == torch.bfloat16
-            and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0 and x.numel() // w.shape[1] >= WGRAD_MIN_ROWS):
+    if _use_linear_fn(x, w):
         return _Linear.apply(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 

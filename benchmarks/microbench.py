@@ -65,11 +65,14 @@ def main():
         t_dx = timeit(lambda: G @ W)
         t_dw = timeit(lambda: G.t() @ A)
         t_k9 = timeit(lambda: ops.wgrad(G, A))
+        t_k9b = timeit(lambda: ops.native().wgrad_bias(G, A))
+        t_k9s = timeit(lambda: (ops.wgrad(G, A), G.sum(0)))
         gemms[name] = {"MNK": [M, N, K], "fwd_tflops": fl / t_f / 1e12,
                        "dgrad_tflops": fl / t_dx / 1e12, "wgrad_tflops": fl / t_dw / 1e12,
                        "wgrad_k9_tflops": fl / t_k9 / 1e12,
                        "fwd_us": t_f * 1e6, "dgrad_us": t_dx * 1e6, "wgrad_us": t_dw * 1e6,
-                       "wgrad_k9_us": t_k9 * 1e6}
+                       "wgrad_k9_us": t_k9 * 1e6, "wgrad_k9_fused_bias_us": t_k9b * 1e6,
+                       "wgrad_k9_plus_torch_bias_us": t_k9s * 1e6}
     res["gemm"] = gemms
     # ---------------- attention ------------------------------------------------------------------
     qkv = (0.5 * torch.randn(T, 3 * H, device=dev)).to(bf).requires_grad_(True)

@@ -339,3 +339,4 @@ def test_linear_autograd_uses_wgrad_kernel():
     rx, rw, rb = torch.autograd.grad(torch.nn.functional.linear(x.float(), w.float(), b.float()),
                                      (x, w, b), g.float())
     _grads_close((gx, gw, gb), (rx, rw, rb), tol=1e-2)
+
