@@ -54,6 +54,8 @@ class FLConfig:
     wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
     server_wire_dtype: str = "fp32"
+    client_lanes: int = 0               # concurrent client lanes per rank (own replica + HIP stream);
+                                        # 0 = auto (min(8, hosted clients) on GPU, 1 on CPU)
     # --- trust layer -------------------------------------------------------------
     anomaly_filter: str = "none"        # none | pagerank | modz | both
     anomaly_k: float = 2.0              # reject below mean - k*std of PageRank

@@ -18,11 +18,13 @@ console lines.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import time
 import zlib
-from typing import Dict, List, Optional
+from dataclasses import dataclass, field
+from typing import Dict, Iterator, List, Optional
 
 import numpy as np
 import torch
@@ -59,6 +61,21 @@ def weighted_average(metrics):
         if vals:
             out[key] = sum(vals) / max(ex, 1)
     return out
+
+
+@dataclass
+class ClientLane:
+    """One concurrent training lane: a model replica with its own flat buffers / optimizer and its
+    own HIP stream. Lanes train different clients at the same time, so the small per-client GEMMs,
+    attention and normalisation kernels of several clients share the 256 CUs instead of each
+    leaving most of the chip idle in its tail (MI355X has 4 hardware queues per process)."""
+    index: int
+    model: torch.nn.Module
+    flat: FlatParams
+    opt: FlatAdamW
+    trainer: LocalTrainer
+    stream: Optional["torch.cuda.Stream"] = None
+    clients: List[int] = field(default_factory=list)
 
 
 class Federation:
@@ -105,6 +122,7 @@ class Federation:
         if cfg.mode == "serverless" and self.multi and not cfg.compat_chain:
             for c in self.local_clients:
                 self.client_master[c] = self.flat.master.detach().clone()
+        self.lanes = self._build_lanes(vocab, mdtype)
         self.global_master: Optional[torch.Tensor] = None
         if cfg.mode == "server":
             self.global_master = self.flat.master.detach().clone()
@@ -148,6 +166,107 @@ class Federation:
         self.provenance_rows = 0
         if cfg.resume:
             self._resume(cfg.resume)
+
+    # ================================ lanes ====================================================
+    def _build_lanes(self, vocab: int, mdtype: torch.dtype) -> List[ClientLane]:
+        cfg = self.cfg
+        if not (cfg.mode == "serverless" and self.multi and not cfg.compat_chain):
+            return []
+        n = cfg.client_lanes or (min(8, len(self.local_clients)) if self.is_cuda else 1)
+        n = max(1, min(n, len(self.local_clients)))
+        lanes = []
+        for i in range(n):
+            if i == 0:
+                model, flat, opt, tr = self.model, self.flat, self.opt, self.trainer
+            else:
+                model = build_model(cfg.model, self.num_labels, device=self.device, dtype=mdtype,
+                                    dropout=cfg.dropout, vocab_size=vocab, seed=cfg.seed,
+                                    lora_rank=cfg.lora_rank, lora_alpha=cfg.lora_alpha)
+                flat = FlatParams.from_model(model, self.device, mdtype)
+                flat.load_master(self.flat.master)
+                opt = FlatAdamW(flat, cfg.lr, cfg.adam_betas, cfg.adam_eps, cfg.weight_decay,
+                                cfg.adam_mode)
+                tr = LocalTrainer(model, flat, opt)
+            stream = torch.cuda.Stream(device=self.device) if self.is_cuda else None
+            lanes.append(ClientLane(i, model, flat, opt, tr, stream,
+                                    list(self.local_clients[i::n])))
+        return lanes
+
+    def _on(self, lane: ClientLane):
+        return torch.cuda.stream(lane.stream) if lane.stream is not None else contextlib.nullcontext()
+
+    @contextlib.contextmanager
+    def _client_rng(self, c: int):
+        g = ops.rng.global_rng()
+        g.load_state(self.client_rng[c])
+        try:
+            yield
+        finally:
+            self.client_rng[c] = g.state()
+
+    def _lane_worker(self, lane: ClientLane, r: int, need_prev: bool, out: dict) -> Iterator[None]:
+        """Generator: trains the lane's clients one after another, yielding after every optimizer
+        step so the round driver can interleave the lanes' launches (streams run concurrently)."""
+        cfg = self.cfg
+        for c in lane.clients:
+            with self._on(lane):
+                lane.flat.load_master(self.client_master[c])
+                if cfg.keep_optimizer_state and c in self.client_opt:
+                    lane.opt.load_state_dict(self.client_opt[c])
+                else:
+                    lane.opt.reset()
+                prev = lane.flat.master.detach().clone() if need_prev else None
+                loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
+            st = {"batches": 0, "tokens": 0, "examples": 0}
+            for e in range(cfg.local_epochs):
+                with self._on(lane):
+                    batches = self.train_batches(c, r, e)
+                for b in batches:
+                    with self._on(lane), self._client_rng(c):
+                        lane.trainer.step(b, loss_acc)
+                    st["batches"] += 1
+                    st["tokens"] += b.real_tokens
+                    st["examples"] += b.batch_size
+                    yield
+            st["loss_t"] = loss_acc
+            self.tokens_trained += st["tokens"]
+            if c in cfg.inject_slow:
+                time.sleep(cfg.inject_slow[c] / 1000.0)
+            with self._on(lane):
+                if prev is not None:
+                    self._inject_byzantine(c, prev, lane.flat)
+                    if self.filter is not None:
+                        out["sk"][c], out["nr"][c] = self._update_stats(prev, lane.flat)
+                out["losses"][c] = st
+                if cfg.eval_local:
+                    out["local_eval"][c] = lane.trainer.evaluate_device(self.test_batches(c, r))
+                out["roots"][c] = (ops.merkle_root_deferred(lane.flat.master)
+                                   if self.ledger is not None else None)
+                self.client_master[c].copy_(lane.flat.master)
+                if cfg.keep_optimizer_state:
+                    self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
+                                          for k, v in lane.opt.state_dict().items()}
+            yield
+
+    def _train_lanes(self, r: int, need_prev: bool) -> dict:
+        """All hosted clients of this rank, trained concurrently on the client lanes."""
+        out = {"sk": {}, "nr": {}, "losses": {}, "local_eval": {}, "roots": {}}
+        main = torch.cuda.current_stream(self.device) if self.is_cuda else None
+        for ln in self.lanes:
+            if ln.stream is not None:
+                ln.stream.wait_stream(main)  # last round's mixing / checkpoint reads are ordered
+        with self.timer.phase("train"):
+            gens = [self._lane_worker(ln, r, need_prev, out) for ln in self.lanes]
+            while gens:
+                for g in list(gens):
+                    try:
+                        next(g)
+                    except StopIteration:
+                        gens.remove(g)
+        for ln in self.lanes:
+            if ln.stream is not None:
+                main.wait_stream(ln.stream)
+        return out
 
     # ================================ helpers ==================================================
     def log(self, *a):
@@ -238,17 +357,18 @@ class Federation:
         return out
 
     @torch.no_grad()
-    def _inject_byzantine(self, c: int, ref: torch.Tensor):
+    def _inject_byzantine(self, c: int, ref: torch.Tensor, flat: Optional[FlatParams] = None):
         s = self.cfg.inject_byzantine.get(c)
         if s is None:
             return
-        m = self.flat.master
+        flat = flat or self.flat
+        m = flat.master
         m.sub_(ref).mul_(s).add_(ref)
-        self.flat.sync_param_from_master()
+        flat.sync_param_from_master()
 
     @torch.no_grad()
-    def _update_stats(self, ref: torch.Tensor):
-        d = self.flat.master - ref
+    def _update_stats(self, ref: torch.Tensor, flat: Optional[FlatParams] = None):
+        d = (flat or self.flat).master - ref
         return ops.block_sketch(d, self.cfg.sketch_dim).float(), d.norm().float()
 
     def _verdicts(self, sk_local: Dict[int, torch.Tensor], nrm_local: Dict[int, torch.Tensor]) -> Verdicts:
@@ -374,7 +494,14 @@ class Federation:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
         need_prev = self.filter is not None or bool(cfg.inject_byzantine)
-        for c in self.local_clients:
+        if self.lanes:
+            o = self._train_lanes(r, need_prev)
+            sk, nr, losses, local_eval = o["sk"], o["nr"], o["losses"], o["local_eval"]
+            for c in self.local_clients:
+                root = ops.root_bytes(o["roots"][c]).hex() if o["roots"][c] is not None else ""
+                recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
+                             "verdict": "accept", "metrics": {"examples": losses[c]["examples"]}})
+        for c in ([] if self.lanes else self.local_clients):
             self._activate(c)
             prev = self.flat.master.detach().clone() if need_prev else None
             st = self._train_client(c, r)

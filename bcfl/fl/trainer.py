@@ -43,21 +43,22 @@ class LocalTrainer:
     def __init__(self, model, flat: FlatParams, opt: FlatAdamW):
         self.model, self.flat, self.opt = model, flat, opt
 
+    def step(self, b: PackedBatch, loss_acc: torch.Tensor) -> None:
+        """One optimizer step on one batch; the loss is accumulated on the device (no sync)."""
+        self.model.train()
+        logits = self.model(b)
+        loss = ops.cross_entropy(logits, b.labels)
+        loss.backward()
+        self.opt.step()
+        self.flat.zero_grad()
+        loss_acc += loss.detach()
+
     def train_epoch(self, batches: Sequence[PackedBatch]) -> Dict[str, torch.Tensor]:
-        m = self.model
-        m.train()
-        dev = self.flat.device
-        loss_acc = torch.zeros((), dtype=torch.float32, device=dev)
-        tokens = 0
+        loss_acc = torch.zeros((), dtype=torch.float32, device=self.flat.device)
         for b in batches:
-            logits = m(b)
-            loss = ops.cross_entropy(logits, b.labels)
-            loss.backward()
-            self.opt.step()
-            self.flat.zero_grad()
-            loss_acc += loss.detach()
-            tokens += b.real_tokens
-        return {"loss_sum": loss_acc, "batches": len(batches), "tokens": tokens,
+            self.step(b, loss_acc)
+        return {"loss_sum": loss_acc, "batches": len(batches),
+                "tokens": sum(b.real_tokens for b in batches),
                 "examples": sum(b.batch_size for b in batches)}
 
     @torch.no_grad()

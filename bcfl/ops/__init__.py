@@ -5,12 +5,13 @@ from .functional import (bias_dropout_add_layernorm, layernorm, bias_act, varlen
                          embedding_layernorm, rmsnorm, rope, swiglu, cross_entropy, linear, dropout,
                          wgrad)
 from .flat import (adamw_, adamw_multi_, gossip_mix_, weighted_accumulate_, block_sketch, scale_, axpby_,
-                   cast_copy_, merkle_root_sha256, leaf_digests_sha256)
+                   cast_copy_, merkle_root_sha256, merkle_root_deferred, root_bytes,
+                   leaf_digests_sha256)
 
 __all__ = [
     "rng", "ref", "native_available", "native", "use_native", "load_error",
     "bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
     "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "dropout", "wgrad",
     "adamw_", "adamw_multi_", "gossip_mix_", "weighted_accumulate_", "block_sketch", "scale_", "axpby_",
-    "cast_copy_", "merkle_root_sha256", "leaf_digests_sha256",
+    "cast_copy_", "merkle_root_sha256", "merkle_root_deferred", "root_bytes", "leaf_digests_sha256",
 ]

@@ -147,3 +147,19 @@ def merkle_root_sha256(buf: torch.Tensor, leaf_bytes: int = LEAF_BYTES_DEFAULT) 
         root = C.sha256_merkle(leaves)
         return bytes(root.cpu().numpy().tobytes())
     return merkle_from_leaves(_leaf_digests_host(_np_bytes(buf), leaf_bytes))
+
+
+def merkle_root_deferred(buf: torch.Tensor, leaf_bytes: int = LEAF_BYTES_DEFAULT):
+    """Like :func:`merkle_root_sha256` but without the host sync: on GPU the 32-byte root stays a
+    device tensor (stream-ordered after the hashing kernels) until :func:`root_bytes` reads it,
+    so concurrent client lanes are never stalled by a per-client readback."""
+    if use_native(buf):
+        C = native()
+        return C.sha256_merkle(C.sha256_leaves(buf, int(leaf_bytes)))
+    return merkle_root_sha256(buf, leaf_bytes)
+
+
+def root_bytes(root) -> bytes:
+    if isinstance(root, (bytes, bytearray)):
+        return bytes(root)
+    return bytes(root.cpu().numpy().tobytes())

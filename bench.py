@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-ckpt", action="store_true")
     ap.add_argument("--out", default=None)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
     return ap.parse_args()
 
 
@@ -59,7 +60,7 @@ def main():
                      num_rounds=a.warmup + a.steps, mode=a.mode, lr=a.lr,
                      async_gossip=not a.sync, ledger=not a.no_ledger,
                      save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
-                     device=a.device)
+                     device=a.device, client_lanes=a.lanes)
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
         fed.run_round(r)
@@ -111,6 +112,7 @@ def main():
                        "clients": a.clients, "mode": a.mode,
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
+                       "client_lanes_per_gpu": len(fed.lanes) or 1,
                        "checkpoint_every_round": cfg.save_every == 1},
             "last_round_phases_s": phases,
         }

@@ -171,3 +171,23 @@ def test_client_count_sweep_cli(tmp_out):
     assert [r["num_clients"] for r in res] == [2, 3]
     for n in (2, 3):
         assert os.path.exists(os.path.join(tmp_out, f"clients_{n}", "metrics.jsonl"))
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_client_lanes_match_sequential(tmp_out, lanes):
+    """Interleaved client lanes (one replica + stream each) reproduce one-lane training exactly:
+    per-client data order, dropout keys and optimizer resets do not depend on the interleaving."""
+    outs = {}
+    for n in (1, lanes):
+        D.set_runtime_for_tests(None)
+        cfg = _cfg(os.path.join(tmp_out, f"l{n}"), mode="serverless", num_clients=4, client_lanes=n,
+                   ledger=True, save_every=0, anomaly_filter="modz", dropout=0.1)
+        fed = Federation(cfg, verbose=False)
+        assert len(fed.lanes) == n
+        h = fed.run()
+        outs[n] = (torch.stack([fed.client_master[c] for c in range(4)]).clone(),
+                   [r["train_loss"] for r in h], [r["global_acc"] for r in h],
+                   [blk["update_root"] for blk in fed.ledger.blocks()])
+    a, b = outs[1], outs[lanes]
+    torch.testing.assert_close(a[0], b[0], atol=0, rtol=0)
+    assert a[1] == pytest.approx(b[1], abs=0) and a[2] == b[2] and a[3] == b[3]
