@@ -19,3 +19,13 @@ Layout::
 """
 
 __version__ = "0.1.0"
+
+import os as _os
+
+# Client lanes run several training steps concurrently on separate HIP streams. hipBLASLt's
+# Stream-K GEMM kernels (SK3) spin-wait on partial tiles produced by other workgroups of the SAME
+# launch; two of them running at once can each hold the CUs the other one's producers need and
+# deadlock (observed: Llama-3-8B LoRA, 2 lanes, GPU 100 % busy, zero memory traffic, forever).
+# Data-parallel Stream-K mode computes whole tiles per workgroup (no cross-workgroup waits).
+# Must be set before the first GEMM initialises the Tensile library.
+_os.environ.setdefault("TENSILE_STREAMK_DATA_PARALLEL", "1")

@@ -37,6 +37,10 @@ def run_sweep(cfg) -> List[dict]:
 
 
 def main(argv: Optional[List[str]] = None, default_preset: Optional[str] = None) -> int:
+    import os
+    if os.environ.get("BCFL_STACKDUMP"):  # periodic all-thread stack dumps (diagnose stalls)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["BCFL_STACKDUMP"]), repeat=True)
     cfg = parse_cli(argv, default_preset=default_preset)
     from .fl import Federation
     from .parallel import dist as D

@@ -54,6 +54,8 @@ class FLConfig:
     wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
     server_wire_dtype: str = "fp32"
+    overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
+                                          # None = auto: on when a rank trains one client at a time
     client_lanes: int = 0               # concurrent client lanes per rank (own replica + HIP stream);
                                         # 0 = auto (min(8, hosted clients) on GPU, 1 on CPU)
     # --- trust layer -------------------------------------------------------------
@@ -82,6 +84,7 @@ class FLConfig:
     log_provenance: bool = True         # per-round sampled train/test indices (reference C18)
     sweep_clients: List[int] = field(default_factory=list)  # run once per client count (C19)
     profile: bool = False
+    progress: bool = False              # per-client / per-round progress lines (long rounds)
     deterministic: bool = False
     seed: int = 42
     device: str = "auto"                # auto | cuda | cpu

@@ -49,6 +49,8 @@ class LocalTrainer:
         logits = self.model(b)
         loss = ops.cross_entropy(logits, b.labels)
         loss.backward()
+        if self.flat.device.type == "cuda":
+            ops.join_wgrad(self.flat.device)  # overlapped weight gradients -> optimizer
         self.opt.step()
         self.flat.zero_grad()
         loss_acc += loss.detach()

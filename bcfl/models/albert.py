@@ -79,6 +79,11 @@ class AlbertForSequenceClassification(SeqClassifierBase):
         self.pooler_bias = new_param((H,), device, dtype, "zeros")
         self.classifier_weight = new_param((cfg.num_labels, H), device, dtype, "normal", std)
         self.classifier_bias = new_param((cfg.num_labels,), device, dtype, "zeros")
+        # applied num_hidden_layers times: autograd sums their gradients, so their weight
+        # gradients must stay on autograd's stream (no side-stream overlap)
+        for p in (self.qkv_weight, self.qkv_bias, self.dense_weight, self.dense_bias,
+                  self.ffn_weight, self.ffn_bias, self.ffn_out_weight, self.ffn_out_bias):
+            p._bcfl_shared = True
 
     def _layer(self, x, batch):
         c, tr = self.cfg, self.training

@@ -50,9 +50,16 @@ def force_torch() -> bool:
     return os.environ.get("BCFL_FORCE_TORCH", "0") == "1"
 
 
-def use_native(t) -> bool:
-    """True when tensor ``t`` must go through the HIP kernels."""
-    return bool(getattr(t, "is_cuda", False)) and not force_torch()
+def _torch_ops():
+    return set(filter(None, os.environ.get("BCFL_TORCH_OPS", "").split(",")))
+
+
+def use_native(t, op: str = "") -> bool:
+    """True when tensor ``t`` must go through the HIP kernels. ``BCFL_TORCH_OPS=attn,rope,...``
+    routes the named ops to the reference path on GPU (bisection / A-B benchmarking only)."""
+    if not bool(getattr(t, "is_cuda", False)) or force_torch():
+        return False
+    return not (op and op in _torch_ops())
 
 
 def load_error():

@@ -39,7 +39,7 @@ def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], 
     param live in flat buffers at ``offsets``: one multi-tensor launch per <=48 tensors."""
     if not grads:
         return
-    if use_native(master):
+    if use_native(master, "adamw"):
         native().adamw_mt(master, m, v, param_out, list(grads), [int(o) for o in offsets],
                           float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
                           int(step), 0 if mode == "hf" else 1, float(grad_scale))

@@ -22,7 +22,8 @@ from . import rng as _rng
 from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
-           "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad"]
+           "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
+           "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
 def _keys(p: float, training: bool):
@@ -48,15 +49,72 @@ def wgrad(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return g2.t().mm(x2)
 
 
+# ----------------------------------------------------------------------------------------
+# Overlapped weight gradients: the backward critical path is the chain of input-gradient GEMMs /
+# attention / LayerNorm backward kernels; the weight gradients hang off it and are only needed
+# by the optimizer. With overlap on, each dW (+db) is launched on a side HIP stream paired with
+# the stream autograd runs on, so the K9 kernels fill the CUs the (often sub-wave) dgrad GEMMs
+# leave idle; :func:`join_wgrad` makes the optimizer's stream wait for them.
+# ----------------------------------------------------------------------------------------
+_WG = {"enabled": False, "side": {}}
+
+
+def set_wgrad_overlap(enabled: bool) -> None:
+    _WG["enabled"] = bool(enabled)
+
+
+def wgrad_overlap_enabled() -> bool:
+    return _WG["enabled"]
+
+
+def _side_stream(cur: "torch.cuda.Stream") -> "torch.cuda.Stream":
+    key = (cur.device_index, cur.cuda_stream)
+    s = _WG["side"].get(key)
+    if s is None:
+        s = _WG["side"][key] = torch.cuda.Stream(device=cur.device)
+    return s
+
+
+def join_wgrad(device=None) -> None:
+    """Current stream waits for the weight gradients launched from it (no-op when none)."""
+    if not _WG["side"]:
+        return
+    cur = torch.cuda.current_stream(device)
+    s = _WG["side"].get((cur.device_index, cur.cuda_stream))
+    if s is not None:
+        cur.wait_stream(s)
+
+
+def _wgrad_async(g2, x2, want_b):
+    cur = torch.cuda.current_stream(g2.device)
+    side = _side_stream(cur)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        if want_b:
+            dw, db = native().wgrad_bias(g2, x2)
+        else:
+            dw, db = native().wgrad(g2, x2), None
+    # operands are freed by autograd when this node returns; results are read on `cur`
+    g2.record_stream(side)
+    x2.record_stream(side)
+    dw.record_stream(cur)
+    if db is not None:
+        db.record_stream(cur)
+    return dw, db
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T (+ b). Forward and input-gradient GEMMs are hipBLASLt (they run at 560-820 TF/s
     on the BERT shapes); the weight gradient — long reduction over tokens, small output — goes
-    to the split-M MFMA kernel (gemm.hip)."""
+    to the split-M MFMA kernel (gemm.hip), optionally on a side stream (overlap)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        # a parameter used several times per step gets its gradients summed by autograd on
+        # autograd's stream, which a side-stream dW would race with
+        ctx.shared = getattr(w, "_bcfl_shared", False) or getattr(b, "_bcfl_shared", False)
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -69,7 +127,10 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = g2.mm(w).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1]:
+        if (ctx.needs_input_grad[1] and _WG["enabled"] and not ctx.shared and use_native(g2)
+                and wgrad_supported(g2, x2)):
+            dw, db = _wgrad_async(g2, x2, want_b)
+        elif ctx.needs_input_grad[1]:
             if want_b and use_native(g2) and wgrad_supported(g2, x2):
                 dw, db = native().wgrad_bias(g2, x2)  # bias gradient fused into the K9 kernel
             else:
@@ -119,7 +180,7 @@ class _BDALN(torch.autograd.Function):
 def bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps: float, p: float = 0.0,
                                training: bool = False):
     p8, ka, kb = _keys(p, training)
-    if use_native(y):
+    if use_native(y, "bdaln"):
         return _BDALN.apply(y.contiguous(), bias, residual, gamma, beta, eps, p8, ka, kb)
     return ref.bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps, p8, ka, kb)
 
@@ -151,7 +212,7 @@ class _BiasAct(torch.autograd.Function):
 
 
 def bias_act(y, bias, act: str = "gelu"):
-    if use_native(y):
+    if use_native(y, "bias_act"):
         return _BiasAct.apply(y.contiguous(), bias, _ACT_ID[act])
     return ref.bias_act(y, bias, act)
 
@@ -186,7 +247,7 @@ def varlen_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, cu_host: Seque
     """qkv: [T, (nh + 2 nkv) * d] (q | k | v column blocks). Returns [T, nh * d]."""
     scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
     p8, ka, kb = _keys(dropout_p, training)
-    if use_native(qkv):
+    if use_native(qkv, "attn"):
         return _VarlenAttn.apply(qkv.contiguous(), cu_seqlens, max_seqlen, num_heads,
                                  num_kv_heads, head_dim, scale, causal, p8, ka, kb)
     return ref.varlen_attention(qkv, num_heads, num_kv_heads, head_dim, cu_host, scale, causal,
@@ -224,7 +285,7 @@ class _EmbLN(torch.autograd.Function):
 def embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps: float,
                         p: float = 0.0, training: bool = False):
     p8, ka, kb = _keys(p, training)
-    if use_native(word_w):
+    if use_native(word_w, "emb_ln"):
         return _EmbLN.apply(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8,
                             ka, kb)
     return ref.embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta,
@@ -249,7 +310,7 @@ class _RMSNorm(torch.autograd.Function):
 
 
 def rmsnorm(x, w, eps: float):
-    if use_native(x):
+    if use_native(x, "rmsnorm"):
         return _RMSNorm.apply(x.contiguous(), w, eps)
     return ref.rmsnorm(x, w, eps)
 
@@ -273,7 +334,7 @@ class _Rope(torch.autograd.Function):
 def rope(qkv: torch.Tensor, pos_ids, cos, sin, num_heads: int, num_kv_heads: int, head_dim: int):
     """Rotate the q and k column blocks of a packed [T, (nh+2nkv)*d] projection (v untouched)."""
     nrot = num_heads + num_kv_heads
-    if use_native(qkv):
+    if use_native(qkv, "rope"):
         return _Rope.apply(qkv.contiguous(), pos_ids, cos, sin, nrot, head_dim)
     T = qkv.shape[0]
     qk = qkv[:, : nrot * head_dim].reshape(T, nrot, head_dim)
@@ -294,7 +355,7 @@ class _SwiGLU(torch.autograd.Function):
 
 
 def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
-    if use_native(gate_up):
+    if use_native(gate_up, "swiglu"):
         return _SwiGLU.apply(gate_up.contiguous())
     return ref.swiglu(gate_up)
 

@@ -44,12 +44,15 @@ def parse():
     ap.add_argument("--out", default=None)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
+    ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    import bcfl  # noqa: F401  (sets the GEMM-library environment before torch initialises it)
     import torch
+    from bcfl import ops
     from bcfl.config import get_preset
     from bcfl.fl import Federation
     from bcfl.parallel import dist as D
@@ -60,7 +63,8 @@ def main():
                      num_rounds=a.warmup + a.steps, mode=a.mode, lr=a.lr,
                      async_gossip=not a.sync, ledger=not a.no_ledger,
                      save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
-                     device=a.device, client_lanes=a.lanes)
+                     device=a.device, client_lanes=a.lanes,
+                     overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad))
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
         fed.run_round(r)
@@ -113,8 +117,10 @@ def main():
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
                        "client_lanes_per_gpu": len(fed.lanes) or 1,
+                       "overlap_wgrad": ops.wgrad_overlap_enabled(),
                        "checkpoint_every_round": cfg.save_every == 1},
             "last_round_phases_s": phases,
+            "hbm_peak_gb": fed.history[-1].get("hbm_peak_gb"),
         }
         print(json.dumps(rec), flush=True)
     D.shutdown()

@@ -191,3 +191,19 @@ def test_client_lanes_match_sequential(tmp_out, lanes):
     a, b = outs[1], outs[lanes]
     torch.testing.assert_close(a[0], b[0], atol=0, rtol=0)
     assert a[1] == pytest.approx(b[1], abs=0) and a[2] == b[2] and a[3] == b[3]
+
+
+def test_client_lanes_share_frozen_lora_base(tmp_out):
+    """LoRA lanes read ONE copy of the frozen base; each lane owns only its adapters."""
+    cfg = _cfg(tmp_out, model="tiny-llama-lora", mode="serverless", num_clients=4, client_lanes=2,
+               num_rounds=1, lr=1e-3, ledger=False, save_every=0)
+    fed = Federation(cfg, verbose=False)
+    a, b = fed.lanes[0].model, fed.lanes[1].model
+    frozen_a = [p for p in a.parameters() if not p.requires_grad]
+    frozen_b = [p for p in b.parameters() if not p.requires_grad]
+    assert frozen_a and all(x is y for x, y in zip(frozen_a, frozen_b))
+    train_a = [p for p in a.parameters() if p.requires_grad]
+    train_b = [p for p in b.parameters() if p.requires_grad]
+    assert all(x.data_ptr() != y.data_ptr() for x, y in zip(train_a, train_b))
+    h = fed.run()
+    assert np.isfinite(h[-1]["train_loss"])

@@ -340,3 +340,31 @@ def test_linear_autograd_uses_wgrad_kernel():
                                      (x, w, b), g.float())
     _grads_close((gx, gw, gb), (rx, rw, rb), tol=1e-2)
 
+
+
+@pytest.mark.parametrize("model", ["bert-base-2l", "albert-base-v2"])
+def test_overlapped_wgrad_matches_inline(model):
+    """Side-stream weight gradients (K9 on a paired stream, joined before the optimizer) give
+    bit-identical parameter gradients to the inline path; ALBERT's shared layer opts out."""
+    from bcfl.data.batching import make_packed_batch
+    from bcfl.data.registry import load_split
+    from bcfl.models import build_model, special_tokens
+    cls_id, sep_id, vocab = special_tokens(model)
+    ds = load_split("imdb", "train", vocab, 512, 1234, cls_id, sep_id)
+    b = make_packed_batch(ds, np.arange(0, 25000, 1563)[:16]).to(DEV)
+    grads = {}
+    for ov in (False, True):
+        ops.set_wgrad_overlap(ov)
+        rng.manual_seed(7)  # identical dropout keys for both passes
+        try:
+            m = build_model(model, 2, device=DEV, dtype=torch.bfloat16, seed=0, dropout=0.0)
+            m.train()
+            loss = ops.cross_entropy(m(b), b.labels)
+            loss.backward()
+            ops.join_wgrad()
+            grads[ov] = [p.grad.clone() for p in m.parameters() if p.grad is not None]
+        finally:
+            ops.set_wgrad_overlap(False)
+    assert len(grads[False]) == len(grads[True])
+    for a, c in zip(grads[False], grads[True]):
+        assert torch.equal(a, c)
