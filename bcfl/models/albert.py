@@ -85,12 +85,18 @@ class AlbertForSequenceClassification(SeqClassifierBase):
                   self.ffn_weight, self.ffn_bias, self.ffn_out_weight, self.ffn_out_bias):
             p._bcfl_shared = True
 
-    def _layer(self, x, batch):
+    def _layer(self, x, batch, rows=None):
         c, tr = self.cfg, self.training
         qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
-        ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
-                                   c.num_attention_heads, c.num_attention_heads, c.head_dim,
-                                   c.attention_probs_dropout_prob, tr)
+        if rows is None:
+            ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
+                                       c.num_attention_heads, c.num_attention_heads, c.head_dim,
+                                       c.attention_probs_dropout_prob, tr)
+        else:  # last application: only the pooled [CLS] rows are consumed
+            ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
+                                             c.num_attention_heads, c.num_attention_heads,
+                                             c.head_dim, c.attention_probs_dropout_prob, tr)
+            x = x.index_select(0, rows.long())
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.dense_weight), self.dense_bias, x,
                                             self.attn_ln_weight, self.attn_ln_bias,
                                             c.layer_norm_eps, c.hidden_dropout_prob, tr)
@@ -107,9 +113,11 @@ class AlbertForSequenceClassification(SeqClassifierBase):
                                     self.emb_ln_bias, c.layer_norm_eps, c.hidden_dropout_prob,
                                     self.training)
         x = ops.linear(e, self.map_weight, self.map_bias)
-        for _ in range(c.num_hidden_layers):
-            x = self._layer(x, batch)
-        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
+        rows = batch.cu_seqlens[:batch.n_seq]
+        for i in range(c.num_hidden_layers):
+            last = i == c.num_hidden_layers - 1 and self.pooled_rows_only
+            x = self._layer(x, batch, rows if last else None)
+        cls = x if self.pooled_rows_only else x.index_select(0, rows.long())
         pooled = torch.tanh(ops.linear(cls, self.pooler_weight, self.pooler_bias))
         if self.training and c.classifier_dropout_prob > 0:
             pooled = ops.dropout(pooled, c.classifier_dropout_prob, True)

@@ -69,13 +69,22 @@ class BertLayer(nn.Module):
         self.out_ln_weight = new_param((H,), device, dtype, "ones")
         self.out_ln_bias = new_param((H,), device, dtype, "zeros")
 
-    def forward(self, x: torch.Tensor, batch: PackedBatch) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, batch: PackedBatch,
+                rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``rows``: compute the layer's output only for these token rows (the pooled [CLS] rows
+        of the last layer; K and V still come from every token)."""
         c = self.cfg
         tr = self.training
         qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
-        ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
-                                   c.num_attention_heads, c.num_attention_heads, c.head_dim,
-                                   c.attention_probs_dropout_prob, tr)
+        if rows is None:
+            ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
+                                       c.num_attention_heads, c.num_attention_heads, c.head_dim,
+                                       c.attention_probs_dropout_prob, tr)
+        else:
+            ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
+                                             c.num_attention_heads, c.num_attention_heads,
+                                             c.head_dim, c.attention_probs_dropout_prob, tr)
+            x = x.index_select(0, rows.long())
         y = ops.linear(ctx, self.attn_out_weight)
         x1 = ops.bias_dropout_add_layernorm(y, self.attn_out_bias, x, self.attn_ln_weight,
                                             self.attn_ln_bias, c.layer_norm_eps,
@@ -128,21 +137,28 @@ class BertForSequenceClassification(SeqClassifierBase):
         self.classifier_weight = new_param((cfg.num_labels, H), device, dtype, "normal", std)
         self.classifier_bias = new_param((cfg.num_labels,), device, dtype, "zeros")
 
-    def encode(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def encode(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None,
+               rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Hidden states of every token ([T, H]); with ``rows``, the last layer only produces
+        those rows ([len(rows), H])."""
         c = self.cfg
         x = ops.embedding_layernorm(batch.input_ids, batch.position_ids, token_type_ids,
                                     self.word_embeddings, self.position_embeddings,
                                     self.token_type_embeddings, self.emb_ln_weight,
                                     self.emb_ln_bias, c.layer_norm_eps, c.hidden_dropout_prob,
                                     self.training)
-        for layer in self.layers:
-            x = layer(x, batch)
+        last = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            x = layer(x, batch, rows if i == last else None)
         return x
 
     def forward(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = self.cfg
-        x = self.encode(batch, token_type_ids)
-        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
+        rows = batch.cu_seqlens[:batch.n_seq]
+        if self.pooled_rows_only:
+            cls = self.encode(batch, token_type_ids, rows)
+        else:
+            cls = self.encode(batch, token_type_ids).index_select(0, rows.long())
         pooled = torch.tanh(ops.linear(cls, self.pooler_weight, self.pooler_bias))
         p = c.classifier_dropout if c.classifier_dropout is not None else c.hidden_dropout_prob
         if self.training and p > 0:

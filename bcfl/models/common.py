@@ -1,6 +1,7 @@
 """Shared model plumbing: parameter init, HF-name mapping, packed-batch helpers."""
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -44,6 +45,9 @@ class SeqClassifierBase(nn.Module):
 
     hf_architecture: str = ""
     hf_model_type: str = ""
+    # The classifier reads one row per sequence ([CLS] / last token), so the last encoder layer
+    # only computes those rows (same logits and gradients; tests compare against False).
+    pooled_rows_only: bool = os.environ.get("BCFL_POOLED_ROWS", "1") == "1"
 
     def forward(self, batch: PackedBatch) -> torch.Tensor:  # logits [B, C]
         raise NotImplementedError

@@ -59,11 +59,17 @@ class DistilBertLayer(nn.Module):
         self.out_ln_weight = new_param((H,), device, dtype, "ones")
         self.out_ln_bias = new_param((H,), device, dtype, "zeros")
 
-    def forward(self, x, batch: PackedBatch):
+    def forward(self, x, batch: PackedBatch, rows=None):
         c, tr = self.cfg, self.training
         qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
-        ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
-                                   c.n_heads, c.n_heads, c.head_dim, c.attention_dropout, tr)
+        if rows is None:
+            ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
+                                       c.n_heads, c.n_heads, c.head_dim, c.attention_dropout, tr)
+        else:  # last layer: only the pooled [CLS] rows are consumed
+            ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
+                                             c.n_heads, c.n_heads, c.head_dim,
+                                             c.attention_dropout, tr)
+            x = x.index_select(0, rows.long())
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.out_lin_weight), self.out_lin_bias,
                                             x, self.sa_ln_weight, self.sa_ln_bias,
                                             c.layer_norm_eps, 0.0, tr)
@@ -118,9 +124,11 @@ class DistilBertForSequenceClassification(SeqClassifierBase):
         x = ops.embedding_layernorm(batch.input_ids, batch.position_ids, None, self.word_embeddings,
                                     self.position_embeddings, None, self.emb_ln_weight,
                                     self.emb_ln_bias, c.layer_norm_eps, c.dropout, self.training)
-        for layer in self.layers:
-            x = layer(x, batch)
-        cls = x.index_select(0, batch.cu_seqlens[:batch.n_seq].long())
+        rows = batch.cu_seqlens[:batch.n_seq]
+        last = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            x = layer(x, batch, rows if (i == last and self.pooled_rows_only) else None)
+        cls = x if self.pooled_rows_only else x.index_select(0, rows.long())
         h = torch.relu(ops.linear(cls, self.pre_classifier_weight, self.pre_classifier_bias))
         if self.training and c.seq_classif_dropout > 0:
             h = ops.dropout(h, c.seq_classif_dropout, True)

@@ -89,7 +89,7 @@ class LlamaLayer(nn.Module):
             self.lora_gate_up = LoRA(H, [I, I], r, a, device, dtype)
             self.lora_down = LoRA(I, [H], r, a, device, dtype)
 
-    def forward(self, x, batch: PackedBatch, cos, sin):
+    def forward(self, x, batch: PackedBatch, cos, sin, rows=None):
         c = self.cfg
         nh, nkv, d = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         h = ops.rmsnorm(x, self.in_ln, c.rms_norm_eps)
@@ -97,8 +97,13 @@ class LlamaLayer(nn.Module):
         if self.lora:
             qkv = qkv + self.lora_qkv(h)
         qkv = ops.rope(qkv, batch.position_ids, cos, sin, nh, nkv, d)
-        ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen, nh, nkv,
-                                   d, 0.0, self.training, causal=True)
+        if rows is None:
+            ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
+                                       nh, nkv, d, 0.0, self.training, causal=True)
+        else:  # last layer: only the pooled last-token rows are consumed
+            ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen, nh,
+                                             nkv, d, 0.0, self.training, causal=True)
+            x = x.index_select(0, rows.long())
         o = ops.linear(ctx, self.o_weight)
         if self.lora:
             o = o + self.lora_o(ctx)
@@ -135,9 +140,12 @@ class LlamaForSequenceClassification(SeqClassifierBase):
 
     def forward(self, batch: PackedBatch, token_type_ids=None):
         x = torch.nn.functional.embedding(batch.input_ids.long(), self.embed_tokens)
-        for layer in self.layers:
-            x = layer(x, batch, self.rope_cos, self.rope_sin)
-        last = x.index_select(0, (batch.cu_seqlens[1:batch.n_seq + 1] - 1).long())
+        rows = batch.cu_seqlens[1:batch.n_seq + 1] - 1
+        n = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            x = layer(x, batch, self.rope_cos, self.rope_sin,
+                      rows if (i == n and self.pooled_rows_only) else None)
+        last = x if self.pooled_rows_only else x.index_select(0, rows.long())
         last = ops.rmsnorm(last, self.norm, self.cfg.rms_norm_eps)
         return ops.linear(last, self.score_weight)
 

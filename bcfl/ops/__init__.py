@@ -2,6 +2,7 @@
 from . import rng, ref
 from ._native import available as native_available, native, use_native, load_error
 from .functional import (bias_dropout_add_layernorm, layernorm, bias_act, varlen_attention,
+                         query_subset_attention,
                          embedding_layernorm, rmsnorm, rope, swiglu, cross_entropy, linear, dropout,
                          wgrad, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad)
 from .flat import (adamw_, adamw_multi_, gossip_mix_, weighted_accumulate_, block_sketch, scale_, axpby_,
@@ -10,7 +11,7 @@ from .flat import (adamw_, adamw_multi_, gossip_mix_, weighted_accumulate_, bloc
 
 __all__ = [
     "rng", "ref", "native_available", "native", "use_native", "load_error",
-    "bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
+    "bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention", "query_subset_attention",
     "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "dropout", "wgrad",
     "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad",
     "adamw_", "adamw_multi_", "gossip_mix_", "weighted_accumulate_", "block_sketch", "scale_", "axpby_",

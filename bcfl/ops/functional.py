@@ -23,7 +23,7 @@ from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
-           "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
+           "query_subset_attention", "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
 def _keys(p: float, training: bool):
@@ -252,6 +252,51 @@ def varlen_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, cu_host: Seque
                                  num_kv_heads, head_dim, scale, causal, p8, ka, kb)
     return ref.varlen_attention(qkv, num_heads, num_kv_heads, head_dim, cu_host, scale, causal,
                                 p8, ka, kb)
+
+
+def query_subset_attention(qkv: torch.Tensor, rows: torch.Tensor, cu_seqlens: torch.Tensor,
+                           max_seqlen: int, num_heads: int, num_kv_heads: int, head_dim: int,
+                           dropout_p: float = 0.0, training: bool = False, causal: bool = False,
+                           scale: Optional[float] = None) -> torch.Tensor:
+    """Attention of ONE query row per sequence (``rows[b]``, an absolute packed-token index inside
+    sequence b) against all keys of sequence b. Returns [B, nh * d].
+
+    Used for the LAST encoder layer of a sequence classifier, whose only consumed output is the
+    pooled row (BERT/ALBERT/DistilBERT: the [CLS] row; Llama: the last token): the layer's other
+    rows feed nothing, so the attention, output projection, FFN and LayerNorms run on B rows
+    instead of T. Same math as :func:`varlen_attention` restricted to those queries, INCLUDING
+    the dropout keep-mask (same element index (t * nh + h) * 8192 + key, same keys drawn), so the
+    logits and every parameter gradient equal the full-layer computation. B x S_max scores: tiny,
+    plain torch ops (autograd) on both devices."""
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    p8, ka, kb = _keys(dropout_p, training)
+    B = int(rows.shape[0])
+    dev = qkv.device
+    nh, nkv, d = num_heads, num_kv_heads, head_dim
+    cu = cu_seqlens[:B + 1].long()
+    starts, lens = cu[:B], cu[1:B + 1] - cu[:B]
+    rows = rows.long()
+    S = max(int(max_seqlen), 1)
+    j = torch.arange(S, device=dev)
+    valid = j[None, :] < lens[:, None]                               # [B, S]
+    if causal:
+        valid = valid & (j[None, :] <= (rows - starts)[:, None])
+    tok = torch.where(valid, starts[:, None] + j[None, :], starts[:, None])
+    cdt = torch.float32
+    q = qkv.index_select(0, rows)[:, : nh * d].reshape(B, nkv, nh // nkv, d).to(cdt)
+    kv = qkv.index_select(0, tok.reshape(-1)).reshape(B, S, -1)[:, :, nh * d:]
+    k = kv[:, :, : nkv * d].reshape(B, S, nkv, d).to(cdt)
+    v = kv[:, :, nkv * d:].reshape(B, S, nkv, d).to(cdt)
+    sc = torch.einsum("bgrd,bsgd->bgrs", q, k) * scale               # [B, nkv, rep, S]
+    sc = sc.masked_fill(~valid[:, None, None, :], float("-inf"))
+    pr = torch.softmax(sc, dim=-1)
+    if p8 > 0:
+        hh = torch.arange(nh, device=dev).reshape(1, nkv, nh // nkv, 1)
+        idx = (rows.reshape(B, 1, 1, 1) * nh + hh) * ref.ATTN_DROP_STRIDE + j.reshape(1, 1, 1, S)
+        keep = _rng.keep_mask_from_index(idx, p8, ka, kb)
+        pr = pr * keep.to(pr.dtype) * _rng.keep_scale(p8)
+    o = torch.einsum("bgrs,bsgd->bgrd", pr, v)
+    return o.reshape(B, nh * d).to(qkv.dtype)
 
 
 # ----------------------------------------------------------------------------------------

@@ -140,3 +140,37 @@ def test_llama8b_lora_trainable_size():
     n = sum(p.numel() for p in m.parameters() if p.requires_grad)
     assert 41_900_000 < n < 42_000_000  # 41.94 M LoRA + 8192 score
     assert len(m.adapter_items()) == 32 * 14 + 1
+
+
+@pytest.mark.parametrize("name", ["tiny-bert", "tiny-albert", "tiny-distilbert", "tiny-llama-lora"])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_pooled_rows_only_last_layer_is_exact(name, p):
+    """The last layer computing only the pooled rows gives the same logits and the same gradient
+    for every parameter as the full last layer (incl. attention-dropout masks)."""
+    from bcfl.ops import rng as _rng
+    from bcfl.data.batching import make_packed_batch
+    from bcfl.data.registry import load_split
+    m = build_model(name, num_labels=3, seed=0, dtype=torch.float32)
+    for mod in m.modules():  # attention-probability dropout only: hidden dropout hashes row ids
+        for attr in ("attention_probs_dropout_prob", "attention_dropout"):
+            if hasattr(getattr(mod, "cfg", None), attr):
+                setattr(mod.cfg, attr, p)
+        for attr in ("hidden_dropout_prob", "dropout", "classifier_dropout_prob", "seq_classif_dropout"):
+            if hasattr(getattr(mod, "cfg", None), attr):
+                setattr(mod.cfg, attr, 0.0)
+    ds = load_split("tiny", "train", 2048, 128)
+    b = make_packed_batch(ds, np.arange(0, 300, 23))
+    out = {}
+    for flag in (False, True):
+        m.pooled_rows_only = flag
+        m.train()
+        _rng.manual_seed(11)
+        for q in m.parameters():
+            q.grad = None
+        logits = m(b)
+        logits.float().pow(2).sum().backward()
+        out[flag] = (logits.detach().clone(), [q.grad.clone() for q in m.parameters() if q.grad is not None])
+    torch.testing.assert_close(out[True][0], out[False][0], atol=1e-5, rtol=1e-4)
+    assert len(out[True][1]) == len(out[False][1])
+    for a, c in zip(out[True][1], out[False][1]):
+        torch.testing.assert_close(a, c, atol=1e-5, rtol=1e-4)
