@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "kernels/kernels.h"
+#include "comm/mailbox.h"
 
 namespace {
 
@@ -499,4 +500,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("block_sketch", &block_sketch);
   m.def("sha256_leaves", &sha256_leaves);
   m.def("sha256_merkle", &sha256_merkle);
+  bcfl_comm::register_mailbox(m);
 }

@@ -96,9 +96,18 @@ def build_kernels(force=False, verbose=False, jobs=8) -> str:
             jobs_list.append([HIPCC, *common, "-ffp-contract=fast", "-munsafe-fp-atomics",
                               *FILE_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o])
     tinc = sum((["-isystem", p] for p in incs + _py_includes()), [])
+    # C++ comm engine (torch-facing HIP: IPC mailboxes)
+    comm = sorted(glob.glob(os.path.join(HERE, "comm", "*.hip")))
+    chdrs = sorted(glob.glob(os.path.join(HERE, "comm", "*.h")))
+    for s in comm:
+        o = os.path.join(BUILD, "comm_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, [s, *chdrs, __file__]):
+            jobs_list.append([HIPCC, *common, *tinc, "-I", HERE, "-DTORCH_EXTENSION_NAME=_C",
+                              "-DTORCH_API_INCLUDE_EXTENSION_H", "-c", s, "-o", o])
     bo = os.path.join(BUILD, "bindings.o")
     objs.append(bo)
-    if force or _stale(bo, [binding, *hdrs, __file__]):
+    if force or _stale(bo, [binding, *hdrs, *chdrs, __file__]):
         jobs_list.append([HIPCC, *common, *tinc, "-DTORCH_EXTENSION_NAME=_C",
                           "-DTORCH_API_INCLUDE_EXTENSION_H", "-c", binding, "-o", bo])
     if jobs_list:

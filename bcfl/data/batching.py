@@ -67,7 +67,9 @@ def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
     if P == 0:
         return b
     ids = torch.cat([b.input_ids, torch.full((P,), pad_id, dtype=torch.int32)])
-    pos = torch.cat([b.position_ids, torch.arange(P, dtype=torch.int32)])
+    # filler positions are all 0: a filler row can be longer than the model's position table
+    # (P < multiple = 256 > 128 positions of the tiny test models) and its values are never read
+    pos = torch.cat([b.position_ids, torch.zeros(P, dtype=torch.int32)])
     cu = np.concatenate([b.cu_host, [T + P]])
     return PackedBatch(ids, pos, torch.from_numpy(cu.astype(np.int32)), b.labels,
                        max(b.max_seqlen, P), b.seq_lens, cu)

@@ -25,7 +25,7 @@ import numpy as np
 
 from .registry import DatasetSpec
 
-__all__ = ["ClientSplit", "partition_clients", "global_test_indices"]
+__all__ = ["ClientSplit", "partition_clients", "global_test_indices", "majority_rate"]
 
 
 @dataclass
@@ -104,7 +104,33 @@ def partition_clients(kind: str, spec: DatasetSpec, train_labels: np.ndarray,
     return splits
 
 
-def global_test_indices(n_test: int, k: int, seed: int, round_idx: Optional[int] = None) -> np.ndarray:
-    """Global-eval draw (ref ``load_data()`` test sample, ``serverless_NonIID_IMDB.py:300-302``)."""
+def global_test_indices(n_test: int, k: int, seed: int, round_idx: Optional[int] = None,
+                        labels: Optional[np.ndarray] = None) -> np.ndarray:
+    """Global-eval draw (ref ``load_data()`` test sample, ``serverless_NonIID_IMDB.py:300-302``).
+
+    The reference draws ``random.sample`` from the *shuffled* HF split, so its draw is balanced in
+    expectation. Our splits are stored label-sorted, and a small uniform draw can be lopsided (a
+    fixed 100-row draw is 61/39 on synthetic IMDB, so a constant predictor scores 0.61). With
+    ``labels`` the draw is **stratified**: each class contributes ``k / num_classes`` rows (the
+    remainder goes to the lowest class ids), so the majority-class rate is ``ceil(k/C)/k``."""
     r = _rng(seed, 7777, 0 if round_idx is None else round_idx + 1)
-    return np.sort(r.choice(n_test, min(k, n_test), replace=False))
+    k = min(k, n_test)
+    if labels is None:
+        return np.sort(r.choice(n_test, k, replace=False))
+    labels = np.asarray(labels)
+    classes = np.unique(labels)
+    per = np.full(len(classes), k // len(classes), dtype=np.int64)
+    per[: k - per.sum()] += 1
+    out = []
+    for c, m in zip(classes, per):
+        pool = np.flatnonzero(labels == c)
+        out.append(r.choice(pool, min(int(m), len(pool)), replace=False))
+    return np.sort(np.concatenate(out)).astype(np.int64)
+
+
+def majority_rate(labels: np.ndarray, idx: np.ndarray) -> float:
+    """Accuracy of the best constant predictor on ``labels[idx]`` (what an untrained model
+    that collapsed onto one class scores)."""
+    if len(idx) == 0:
+        return 0.0
+    return float(np.bincount(np.asarray(labels)[idx]).max() / len(idx))

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import functools
 from dataclasses import dataclass
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 from .synthetic import TokenDataset, make_synthetic_split
 
@@ -62,16 +62,21 @@ def get_dataset(name: str) -> DatasetSpec:
 
 @functools.lru_cache(maxsize=16)
 def load_split(name: str, split: str, vocab_size: int, max_len: int = 512, seed: int = 1234,
-               cls_id: int = 101, sep_id: int = 102) -> TokenDataset:
+               cls_id: int = 101, sep_id: int = 102,
+               signal: Optional[float] = None) -> TokenDataset:
+    """``signal``: planted own-class tokens per 64 body tokens (None = generator default 3.0;
+    other-class tokens stay at 1.0 per 64) — the difficulty knob of the synthetic task."""
     spec = get_dataset(name)
     if name in TEXT_DATASETS:
         from .text import load_csv_split
         return load_csv_split(name, split, vocab_size, max_len, cls_id, sep_id)
     n = spec.n_train if split == "train" else spec.n_test
     split_seed = seed * 7919 + (0 if split == "train" else 1)
+    kw = {} if signal is None else {"own_signal_rate": float(signal)}
     return make_synthetic_split(n, spec.num_classes, vocab_size, seed=split_seed,
                                 length_median=spec.length_median, length_sigma=spec.length_sigma,
-                                max_len=max_len, cls_id=cls_id, sep_id=sep_id, class_seed=seed)
+                                max_len=max_len, cls_id=cls_id, sep_id=sep_id, class_seed=seed,
+                                **kw)
 
 
 def splits(name: str, vocab_size: int, max_len: int = 512, seed: int = 1234,

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import contextlib
 import json
+import math
 import os
 import time
 import zlib
@@ -33,12 +34,12 @@ from .. import ops
 from ..ckpt import AsyncCheckpointer, dir_size_gb, mirror_dir, load_into
 from ..config import FLConfig
 from ..data.batching import ClientLoader
-from ..data.partition import global_test_indices, partition_clients
+from ..data.partition import global_test_indices, majority_rate, partition_clients
 from ..data.registry import get_dataset, load_split
 from ..models import build_model, model_config, special_tokens
 from ..parallel import dist as D
 from ..parallel.flat import FlatAdamW, FlatParams
-from ..parallel.gossip import GossipEngine
+from ..parallel.gossip import GossipEngine, MailboxGossip
 from ..parallel.topology import clients_of_rank, mixing_matrix, neighbours
 from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
@@ -107,8 +108,10 @@ class Federation:
         vocab = cfg.vocab_size or vocab
         _, mcfg = model_config(cfg.model)
         self.max_len = min(cfg.max_seq_len, getattr(mcfg, "max_position_embeddings", cfg.max_seq_len))
-        self.train_ds = load_split(cfg.dataset, "train", vocab, self.max_len, DATA_SEED, cls_id, sep_id)
-        self.test_ds = load_split(cfg.dataset, "test", vocab, self.max_len, DATA_SEED, cls_id, sep_id)
+        self.train_ds = load_split(cfg.dataset, "train", vocab, self.max_len, DATA_SEED, cls_id,
+                                   sep_id, cfg.synthetic_signal)
+        self.test_ds = load_split(cfg.dataset, "test", vocab, self.max_len, DATA_SEED, cls_id,
+                                  sep_id, cfg.synthetic_signal)
         self.num_labels = cfg.num_labels or self.spec.num_classes
         self._parts: Dict[int, list] = {}
         # ---------------- model + flat buffers ------------------------------------------------
@@ -144,6 +147,16 @@ class Federation:
             self.global_master = self.flat.master.detach().clone()
             self.acc = torch.zeros_like(self.flat.master)
         # ---------------- gossip -------------------------------------------------------------------
+        if cfg.gossip_transport not in ("auto", "mailbox", "rccl"):
+            raise ValueError(f"unknown gossip_transport {cfg.gossip_transport!r}")
+        self.transport = cfg.gossip_transport
+        if self.transport == "auto":
+            self.transport = "mailbox" if cfg.async_gossip else "rccl"
+        # A mailbox federation never waits on a peer: the per-round path is collective-free
+        # (metrics, evaluation and ledger are rank-local) so a slow or exited rank cannot stall
+        # the others. The update anomaly filter needs a global view and keeps its collectives.
+        self.collective_free = (cfg.mode == "serverless" and self.transport == "mailbox"
+                                and cfg.anomaly_filter == "none" and not cfg.compat_chain)
         self.excluded: List[int] = []
         self.gossip: Optional[GossipEngine] = None
         if cfg.mode == "serverless" and not cfg.compat_chain:
@@ -153,12 +166,21 @@ class Federation:
             self.nbrs = neighbours(cfg.topology, n, self.excluded)
             states = ({c: self.client_master[c] for c in self.local_clients} if self.multi
                       else {self.local_clients[0]: self.flat.master})
-            wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
-            if cfg.wire_dtype == "bf16_raw":
-                wire = "bf16"
-            self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip,
-                                       liveness_timeout=cfg.liveness_timeout)
+            if self.transport == "mailbox":
+                self.gossip = MailboxGossip(n, states, self.nbrs,
+                                            "fp32" if cfg.wire_dtype == "fp32" else "bf16",
+                                            sync=not cfg.async_gossip,
+                                            liveness_timeout=cfg.liveness_timeout,
+                                            verify=cfg.verify_updates)
+            else:
+                wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
+                if cfg.wire_dtype == "bf16_raw":
+                    wire = "bf16"
+                self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip,
+                                           liveness_timeout=cfg.liveness_timeout,
+                                           verify=cfg.verify_updates)
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
+            self.gossip.tamper = set(cfg.inject_tamper) & set(self.local_clients)
             self.gossip.seed_replicas(self.flat.master)
         # ---------------- trust ---------------------------------------------------------------------
         self.filter = UpdateAnomalyFilter(cfg.anomaly_filter, cfg.anomaly_k,
@@ -167,7 +189,7 @@ class Federation:
         out = cfg.out_dir
         self.ledger = Ledger(genesis={"model": cfg.model, "mode": cfg.mode, "clients": n,
                                       "dataset": cfg.dataset, "partition": cfg.partition},
-                             path=os.path.join(out, "ledger.jsonl") if (cfg.ledger and self.rt.is_main) else None,
+                             path=self._ledger_path() if cfg.ledger else None,
                              ts=0.0) if cfg.ledger else None
         # ---------------- io ---------------------------------------------------------------------------
         self.metrics = MetricsWriter(os.path.join(out, "metrics.jsonl"),
@@ -178,10 +200,20 @@ class Federation:
         self.global_accuracies: List[float] = []
         self.history: List[dict] = []
         self.start_round = 0
+        self.ledger_audit: Optional[Dict[str, int]] = None
         self.tokens_trained = 0
         self.provenance_rows = 0
         if cfg.resume:
             self._resume(cfg.resume)
+
+    def _ledger_path(self) -> Optional[str]:
+        """Collective mode: one canonical chain, written by rank 0. Collective-free (mailbox)
+        mode: every rank keeps its own chain (rank 0 -> ledger.jsonl, rank k -> ledger.rank{k}.jsonl)."""
+        if self.rt.is_main:
+            return os.path.join(self.cfg.out_dir, "ledger.jsonl")
+        if self.collective_free:
+            return os.path.join(self.cfg.out_dir, f"ledger.rank{self.rt.rank}.jsonl")
+        return None
 
     # ================================ lanes ====================================================
     def _build_lanes(self, vocab: int, mdtype: torch.dtype) -> List[ClientLane]:
@@ -247,6 +279,7 @@ class Federation:
                 with self._on(lane):
                     batches = self.train_batches(c, r, e)
                 for b in batches:
+                    lane.opt.lr = self.lr_at(r, st["batches"])
                     with self._on(lane), self._client_rng(c):
                         lane.trainer.step(b, loss_acc)
                     st["batches"] += 1
@@ -272,7 +305,7 @@ class Federation:
                 if cfg.eval_local:
                     out["local_eval"][c] = lane.trainer.evaluate_device(self.test_batches(c, r))
                 out["roots"][c] = (ops.merkle_root_deferred(lane.flat.master)
-                                   if self.ledger is not None else None)
+                                   if self.ledger is not None and not self._gossip_roots else None)
                 self.client_master[c].copy_(lane.flat.master)
                 if cfg.keep_optimizer_state:
                     self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
@@ -314,6 +347,32 @@ class Federation:
                                                   c.dirichlet_alpha)}
         return self._parts[key]
 
+    @property
+    def steps_per_round(self) -> int:
+        c = self.cfg
+        return c.local_epochs * -(-min(c.train_samples, len(self.train_ds)) // c.batch_size)
+
+    def lr_at(self, r: int, i: int) -> float:
+        """Learning rate of local step ``i`` of round ``r``. Every client follows the same
+        schedule over the run's global local-step index g = r * steps_per_round + i (linear
+        warm-up, then constant / linear / cosine decay to ``lr_min_ratio * lr``)."""
+        c = self.cfg
+        if c.lr_schedule == "constant" and c.lr_warmup_steps <= 0:
+            return c.lr
+        g = r * self.steps_per_round + i
+        if g < c.lr_warmup_steps:
+            return c.lr * (g + 1) / c.lr_warmup_steps
+        if c.lr_schedule == "constant":
+            return c.lr
+        total = max(c.num_rounds * self.steps_per_round - c.lr_warmup_steps, 1)
+        t = min(max((g - c.lr_warmup_steps) / total, 0.0), 1.0)
+        lo = c.lr * c.lr_min_ratio
+        if c.lr_schedule == "linear":
+            return lo + (c.lr - lo) * (1.0 - t)
+        if c.lr_schedule == "cosine":
+            return lo + (c.lr - lo) * 0.5 * (1.0 + math.cos(math.pi * t))
+        raise KeyError(f"unknown lr_schedule {c.lr_schedule!r}")
+
     def client_examples(self, c: int, r: int) -> int:
         return int(len(self.partitions(r)[c].train))
 
@@ -342,10 +401,21 @@ class Federation:
         return ClientLoader(self.test_ds, sp.test, self.cfg.batch_size,
                             pad_multiple=self.pad_multiple).device_batches(self.device)
 
+    def global_test_idx(self, r: int) -> np.ndarray:
+        c = self.cfg
+        return global_test_indices(len(self.test_ds), c.global_test_samples, c.seed,
+                                   r if c.resample_each_round else None,
+                                   self.test_ds.labels if c.global_test_stratified else None)
+
+    def global_majority_rate(self, r: int) -> float:
+        """Best constant-predictor accuracy on round r's global draw (printed beside accuracy so
+        a collapsed model cannot pass for a trained one)."""
+        return majority_rate(self.test_ds.labels, self.global_test_idx(r))
+
     def global_test_batches(self, r: int):
-        idx = global_test_indices(len(self.test_ds), self.cfg.global_test_samples, self.cfg.seed,
-                                  r if self.cfg.resample_each_round else None)
-        mine = idx[self.rt.rank::self.rt.world]
+        idx = self.global_test_idx(r)
+        # collective-free: every rank scores its own model on the whole draw (no all-reduce)
+        mine = idx if self.collective_free else idx[self.rt.rank::self.rt.world]
         if len(mine) == 0:
             return []
         return ClientLoader(self.test_ds, mine, self.cfg.batch_size,
@@ -377,7 +447,8 @@ class Federation:
             with self.timer.phase("data"):
                 batches = self.train_batches(c, r, e)
             with self.timer.phase("train"):
-                res = self.trainer.train_epoch(batches)
+                res = self.trainer.train_epoch(
+                    batches, lr_fn=lambda i, e=e: self.lr_at(r, e * len(batches) + i))
             loss_t = res["loss_sum"] if loss_t is None else loss_t + res["loss_sum"]
             for k in ("batches", "tokens", "examples"):
                 out[k] += res[k]
@@ -419,24 +490,33 @@ class Federation:
         return ops.merkle_root_sha256(self.flat.master).hex()
 
     def _ledger_round(self, r: int, recs: List[dict], extra: Optional[dict] = None):
+        """Append this round's blocks. Collective mode: every rank appends the all-gathered
+        records in one canonical order and the tips are compared across ranks every round
+        (``consensus_check``; divergence aborts). Collective-free (mailbox) mode: each rank
+        chains what it published and verified; chains are cross-audited in :meth:`finish`."""
         if self.ledger is None:
             return
         with self.timer.phase("ledger"):
-            allrecs = [x for part in D.all_gather_object(recs) for x in part]
-            allrecs.sort(key=lambda x: x["client"])
+            allrecs = recs if self.collective_free else [x for part in D.all_gather_object(recs)
+                                                         for x in part]
+            allrecs = sorted(allrecs, key=lambda x: (x["client"], x.get("kind", "update"),
+                                                     x.get("metrics", {}).get("receiver_rank", -1)))
             for x in allrecs:
-                self.ledger.append(r, x["client"], "update", x["root"], x["verdict"],
+                self.ledger.append(r, x["client"], x.get("kind", "update"), x["root"], x["verdict"],
                                    x.get("metrics", {}), ts=x["ts"])
             if extra is not None:
                 self.ledger.append(r, -1, extra.pop("kind", "round"), extra.pop("root", ""),
                                    "accept", extra, ts=float(r + 1))
             self.ledger.flush()
+            if not self.collective_free and self.rt.distributed and not self.ledger.consensus_check():
+                raise RuntimeError(f"ledger tips diverged across ranks at round {r}")
 
     def _eval_global(self, r: int) -> EvalResult:
         with self.timer.phase("eval_global"):
             gb = self.global_test_batches(r)
             acc = self.trainer.evaluate_device(gb) if gb else torch.zeros(4, dtype=torch.float64, device=self.device)
-            D.all_reduce_(acc)
+            if not self.collective_free:
+                D.all_reduce_(acc)
             a = acc.cpu().tolist()
         return EvalResult(int(a[0]), int(a[1]), a[2], a[3])
 
@@ -507,6 +587,37 @@ class Federation:
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                 "client_metrics": client_metrics, "bytes_sent": float(self.flat.nbytes("master"))}
 
+    @property
+    def _gossip_roots(self) -> bool:
+        """The gossip engine hashes every published payload (its ledger commitment), so the
+        update blocks use those roots and the trainer does not hash the master a second time."""
+        return isinstance(getattr(self, "gossip", None), MailboxGossip) and self.gossip.verify
+
+    def _gossip_records(self, r: int, recs: List[dict]) -> List[dict]:
+        """Ledger records from the last exchange: published payload roots replace the update
+        roots; every verified receive becomes a ``verify`` block (verdict accept / reject)."""
+        out = []
+        by_client = {x["client"]: x for x in recs}
+        for g in getattr(self.gossip, "records", []):
+            if g["kind"] == "update":
+                if g.get("root_t") is not None and g["client"] in by_client and self._gossip_roots:
+                    by_client[g["client"]]["root"] = ops.root_bytes(g["root_t"]).hex()
+                if g["client"] in by_client:
+                    by_client[g["client"]].setdefault("metrics", {})["version"] = g["version"]
+            elif g["kind"] == "recv":
+                out.append({"client": g["client"], "kind": "verify", "root": g["root"],
+                            "verdict": "accept" if g["ok"] else "reject",
+                            "ts": float(r) + 0.5 + 0.001 * (g["client"] + 1),
+                            "metrics": {"receiver_rank": self.rt.rank, "version": g["version"],
+                                        "src_round": g["src_round"],
+                                        **({} if g["ok"] else {"reason": "merkle root mismatch"})}})
+        return out
+
+    def _gather_metrics(self, loc: list) -> list:
+        if self.collective_free:
+            return list(loc)
+        return [x for part in D.all_gather_object(loc) for x in part]
+
     def _reduce_train_loss(self, losses: Dict[int, dict]) -> float:
         if not losses:
             return 0.0
@@ -515,7 +626,8 @@ class Federation:
             if st["loss_t"] is not None:
                 t[0] += st["loss_t"].double()
             t[1] += st["batches"]
-        D.all_reduce_(t)
+        if not self.collective_free:
+            D.all_reduce_(t)
         a = t.cpu().tolist()
         return a[0] / max(a[1], 1)
 
@@ -545,7 +657,7 @@ class Federation:
             if cfg.eval_local:
                 with self.timer.phase("eval_local"):
                     local_eval[c] = self.trainer.evaluate_device(self.test_batches(c, r))
-            root = self._merkle() if self.ledger is not None else ""
+            root = self._merkle() if self.ledger is not None and not self._gossip_roots else ""
             recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
                          "verdict": "accept", "metrics": {"examples": st["examples"]}})
             self._deactivate(c)
@@ -559,6 +671,7 @@ class Federation:
         with self.timer.phase("comm"):
             info = self.gossip.end_of_round(r, W, None if self.multi else {self.local_clients[0]: self.flat.param},
                                             steps={c: losses[c]["batches"] for c in losses})
+        recs += self._gossip_records(r, recs)
         self.prev_verdicts = v
         if self.multi:  # evaluate this rank's first client's mixed model
             self.flat.load_master(self.client_master[self.local_clients[0]])
@@ -568,7 +681,7 @@ class Federation:
             a = t.cpu().tolist()
             e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
             loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
-        client_metrics = [x for part in D.all_gather_object(loc) for x in part] if cfg.eval_local else []
+        client_metrics = self._gather_metrics(loc) if cfg.eval_local else []
         if self.verbose and cfg.reference_prints:
             for c, _, m in sorted(client_metrics):
                 print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
@@ -581,7 +694,8 @@ class Federation:
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                 "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
                 "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
-                "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0)}
+                "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
+                "rejected_msgs": info.get("rejected_msgs", 0.0)}
 
     def _chain_round(self, r: int) -> dict:
         """Reference C14 exactly: clients train one after another on ONE shared model; the
@@ -636,6 +750,8 @@ class Federation:
             if self.verbose and self.cfg.reference_prints:
                 print(f"Global Model Accuracy: {gacc * 100:.2f}%", flush=True)
         rec = {"round": r, "mode": self.cfg.mode, "t_round": t_round, "global_acc": gacc,
+               "global_majority_rate": self.global_majority_rate(r) if gacc is not None else None,
+               "global_eval_rows": int(ge.count) if ge is not None else 0,
                "global_loss": ge.loss if ge is not None else None,
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
@@ -684,7 +800,35 @@ class Federation:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
-    def finish(self):
+    def audit_ledgers(self) -> Dict[str, int]:
+        """Cross-rank audit of the per-rank chains of a collective-free federation: every update
+        a rank ACCEPTED must carry exactly the Merkle root its sender committed for that version."""
+        mine = self.ledger.blocks()
+        chains = D.all_gather_object(mine)
+        committed = {}
+        for ch in chains:
+            for b in ch:
+                if b["kind"] == "update":
+                    v = json.loads(b["payload"] or "{}").get("version")
+                    if v is not None:
+                        committed[(b["client"], v)] = b["update_root"]
+        checked = mismatched = rejected = 0
+        for ch in chains:
+            for b in ch:
+                if b["kind"] != "verify":
+                    continue
+                if b["verdict"] != "accept":
+                    rejected += 1
+                    continue
+                key = (b["client"], json.loads(b["payload"] or "{}").get("version"))
+                if key in committed:
+                    checked += 1
+                    mismatched += int(committed[key] != b["update_root"])
+        return {"checked": checked, "mismatched": mismatched, "rejected": rejected}
+
+    def finish(self, audit: bool = True):
+        """Drain communication and I/O, verify the ledger (collective-free runs: cross-rank audit,
+        a collective — pass ``audit=False`` when some rank has exited)."""
         self.drain()
         if self.ckpt is not None:
             self.ckpt.close()
@@ -694,6 +838,11 @@ class Federation:
             bad = self.ledger.verify()
             if bad != -1:
                 raise RuntimeError(f"ledger verification failed at height {bad}")
+            if self.collective_free and self.rt.distributed and audit:
+                self.ledger_audit = self.audit_ledgers()
+                if self.ledger_audit["mismatched"]:
+                    raise RuntimeError(f"ledger audit: {self.ledger_audit['mismatched']} accepted "
+                                       "updates do not match their sender's commitment")
         tel = self.telemetry.finish()
         if self.verbose and self.cfg.reference_prints:
             gdir = os.path.join(self.cfg.out_dir, "global")

@@ -55,9 +55,11 @@ class LocalTrainer:
         self.flat.zero_grad()
         loss_acc += loss.detach()
 
-    def train_epoch(self, batches: Sequence[PackedBatch]) -> Dict[str, torch.Tensor]:
+    def train_epoch(self, batches: Sequence[PackedBatch], lr_fn=None) -> Dict[str, torch.Tensor]:
         loss_acc = torch.zeros((), dtype=torch.float32, device=self.flat.device)
-        for b in batches:
+        for i, b in enumerate(batches):
+            if lr_fn is not None:
+                self.opt.lr = lr_fn(i)
             self.step(b, loss_acc)
         return {"loss_sum": loss_acc, "batches": len(batches),
                 "tokens": sum(b.real_tokens for b in batches),

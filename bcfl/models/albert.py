@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..data.batching import PackedBatch
-from .common import SeqClassifierBase, new_param, row_slice, whole
+from .common import SeqClassifierBase, new_param, row_slice, whole, check_positions
 
 
 @dataclass
@@ -107,6 +107,7 @@ class AlbertForSequenceClassification(SeqClassifierBase):
 
     def forward(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None):
         c = self.cfg
+        check_positions(batch, c.max_position_embeddings)
         e = ops.embedding_layernorm(batch.input_ids, batch.position_ids, token_type_ids,
                                     self.word_embeddings, self.position_embeddings,
                                     self.token_type_embeddings, self.emb_ln_weight,

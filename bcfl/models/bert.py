@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..data.batching import PackedBatch
-from .common import SeqClassifierBase, new_param, row_slice, whole
+from .common import SeqClassifierBase, new_param, row_slice, whole, check_positions
 
 
 @dataclass
@@ -142,6 +142,7 @@ class BertForSequenceClassification(SeqClassifierBase):
         """Hidden states of every token ([T, H]); with ``rows``, the last layer only produces
         those rows ([len(rows), H])."""
         c = self.cfg
+        check_positions(batch, c.max_position_embeddings)
         x = ops.embedding_layernorm(batch.input_ids, batch.position_ids, token_type_ids,
                                     self.word_embeddings, self.position_embeddings,
                                     self.token_type_embeddings, self.emb_ln_weight,

@@ -25,6 +25,16 @@ def new_param(shape, device=None, dtype=torch.float32, init: str = "normal", std
     return nn.Parameter(t, requires_grad=requires_grad)
 
 
+def check_positions(batch: PackedBatch, max_positions: int) -> None:
+    """Host-side bound check before a position-table gather on the GPU: real rows use positions
+    0..len-1 (filler rows use 0), so the longest real row must fit the table — an out-of-range
+    position would be an out-of-bounds read in the embedding kernel and an out-of-bounds write in
+    its backward."""
+    n = int(batch.seq_lens.max()) if len(batch.seq_lens) else 0
+    if n > max_positions:
+        raise ValueError(f"sequence of {n} tokens exceeds the model's {max_positions} positions")
+
+
 def padded_to_packed(b: PaddedBatch, device=None) -> PackedBatch:
     """Convert an HF-style padded batch (right padding) into a packed batch."""
     import numpy as np

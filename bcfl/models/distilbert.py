@@ -14,7 +14,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..data.batching import PackedBatch
-from .common import SeqClassifierBase, new_param, row_slice, whole
+from .common import SeqClassifierBase, new_param, row_slice, whole, check_positions
 
 
 @dataclass
@@ -121,6 +121,7 @@ class DistilBertForSequenceClassification(SeqClassifierBase):
 
     def forward(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None):
         c = self.cfg
+        check_positions(batch, c.max_position_embeddings)
         x = ops.embedding_layernorm(batch.input_ids, batch.position_ids, None, self.word_embeddings,
                                     self.position_embeddings, None, self.emb_ln_weight,
                                     self.emb_ln_bias, c.layer_norm_eps, c.dropout, self.training)

@@ -17,9 +17,12 @@ What this engine does, per round, for every client ``c`` hosted on this rank:
 3. **mix** — x_c <- W_cc x_c + sum_j W_cj view_j   (one fp32 kernel over the flat buffer), where
    ``view_j`` is the latest *published* state of neighbour j (stale by one round when async).
 
-Message integrity and liveness: every published state carries a
-4-word header ``[version, round, steps, version]`` (seqlock layout — a torn message shows different
-head / tail versions) exchanged in the same grouped batch. A receiver applies a bf16 delta to its
+Message integrity and liveness: every published state carries an
+8-word header ``[version, round, steps, root0..root3, version]`` (seqlock layout — a torn message
+shows different head / tail versions; ``root`` = SHA-256 Merkle root of the wire payload, the
+sender's ledger commitment) exchanged in the same grouped batch. The receiver re-hashes every
+payload on its GPU and rejects one whose root differs (tampering in flight; a rejected delta
+breaks the replica chain, so its sender is treated as dead). A receiver applies a bf16 delta to its
 replica only for ``version == applied + 1`` (a repeated or skipped version never double-applies or
 silently drops an increment), and a neighbour whose version has not advanced for more than
 ``liveness_timeout`` rounds is treated as dead: its mixing weight moves to the receiving client's
@@ -43,7 +46,7 @@ from .topology import client_rank
 class GossipEngine:
     def __init__(self, num_clients: int, states: Dict[int, torch.Tensor], nbrs: Dict[int, List[int]],
                  wire: str = "bf16_delta", async_gossip: bool = True, rank: Optional[int] = None,
-                 world: Optional[int] = None, liveness_timeout: int = 2):
+                 world: Optional[int] = None, liveness_timeout: int = 2, verify: bool = True):
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
         self.world = rt.world if world is None else world
@@ -81,7 +84,12 @@ class GossipEngine:
         self.version = {c: 0 for c in self.local}            # last published version per local client
         self.steps = {c: 0 for c in self.local}
         self.suppressed: set = set()                          # fault injection: clients that stop publishing
-        hz = lambda: torch.zeros(4, dtype=torch.int64, device=self.device)  # noqa: E731
+        self.tamper: set = set()      # fault injection: corrupt these clients' payloads after hashing
+        self.verify = verify
+        self.records: List[dict] = []  # ledger records of the last exchange (published + verified)
+        self.rejected_msgs = 0
+        self._pub_roots: Dict[int, object] = {}
+        hz = lambda: torch.zeros(8, dtype=torch.int64, device=self.device)  # noqa: E731
         self.send_hdr = {c: hz() for c in self.local}
         self.recv_hdr = {j: hz() for j in self.remote_needed}
         self.applied = {j: 0 for j in self.remote_needed}     # replica version per remote client
@@ -118,13 +126,21 @@ class GossipEngine:
             self.version[c] += 1
             self.steps[c] += int((steps or {}).get(c, 0))
             v = self.version[c]
-            self.send_hdr[c].copy_(torch.tensor([v, round_idx, self.steps[c], v], dtype=torch.int64))
+            self.send_hdr[c].copy_(torch.tensor([v, round_idx, self.steps[c], 0, 0, 0, 0, v],
+                                                dtype=torch.int64))
             x = self.states[c]
             if self.wire == "bf16_delta":
                 ops.native().delta_encode(x, self.ref[c], self.send_buf[c]) if ops.use_native(x) \
                     else _delta_encode_ref(x, self.ref[c], self.send_buf[c])
             else:
                 ops.cast_copy_(self.send_buf[c], x)
+            if self.verify and self.send_plan:
+                rt_ = ops.merkle_root_deferred(self.send_buf[c])
+                self._pub_roots[c] = rt_
+                rtt = rt_ if torch.is_tensor(rt_) else torch.frombuffer(bytearray(rt_), dtype=torch.uint8)
+                self.send_hdr[c][3:7].copy_(rtt.view(torch.int64))
+                if c in self.tamper:  # in-flight corruption AFTER the commitment was computed
+                    self.send_buf[c][: min(64, self.numel)].add_(1.0)
 
     def launch(self, round_idx: int):
         sends = [(self.send_buf[c], r) for c, r in self.send_plan]
@@ -144,10 +160,28 @@ class GossipEngine:
         rnd = self.pending_round if self.pending_round is not None else 0
         hdrs = (torch.stack([self.recv_hdr[j] for j in self.remote_needed]).cpu().tolist()
                 if self.remote_needed else [])
-        for j, (v0, _r, _steps, v1) in zip(self.remote_needed, hdrs):
+        roots = ({j: ops.merkle_root_deferred(self.recv_buf[j]) for j in self.remote_needed}
+                 if self.verify else {})
+        for c, rt_ in self._pub_roots.items():
+            self.records.append({"client": c, "kind": "update", "version": self.version[c],
+                                 "root_t": rt_})
+        self._pub_roots = {}
+        for j, h in zip(self.remote_needed, hdrs):
+            v0, _r, _steps, v1 = h[0], h[1], h[2], h[7]
             if v0 != v1:  # torn message: keep the previous replica
                 self.torn += 1
                 continue
+            if self.verify and v0 > self.seen_version[j]:
+                claimed = np.asarray(h[3:7], dtype="<i8").tobytes()
+                good = ops.root_bytes(roots[j]) == claimed
+                self.records.append({"client": j, "kind": "recv", "version": v0,
+                                     "root": claimed.hex(), "ok": good, "src_round": _r})
+                if not good:
+                    self.rejected_msgs += 1
+                    if self.wire == "bf16_delta":  # the replica chain of j is broken
+                        self.dead.add(j)
+                        self.applied[j] = -1
+                    continue
             if self.wire == "bf16_delta":
                 if v0 == self.applied[j] + 1:
                     ops.axpby_(self.replica[j], self.recv_buf[j], 1.0, 1.0)
@@ -194,6 +228,7 @@ class GossipEngine:
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
         """Sync: publish -> exchange -> wait -> mix.  Async: wait(prev) -> mix -> publish -> launch."""
         info = {"mixed": 0.0, "stale_rounds": 0.0}
+        self.records = []
         if not self.async_gossip:
             self.publish(round_idx, steps)
             self.launch(round_idx)
@@ -212,10 +247,14 @@ class GossipEngine:
         info["bytes_sent"] = float(self.bytes_sent_last)
         info["dead_peers"] = float(len(self.dead))
         info["torn"] = float(self.torn)
+        info["rejected_msgs"] = float(self.rejected_msgs)
         return info
 
     def drain(self):
         self.finish()
+
+    def close(self):
+        self.drain()
 
 
 @torch.no_grad()
@@ -223,3 +262,192 @@ def _delta_encode_ref(x: torch.Tensor, ref: torch.Tensor, out: torch.Tensor):
     q = (x - ref).to(out.dtype)
     out.copy_(q)
     ref.add_(q.float())
+
+
+class MailboxGossip:
+    """Truly asynchronous serverless gossip over one-sided peer mailboxes
+    (:mod:`bcfl.parallel.mailbox`): no matched receive, no round lock-step.
+
+    Per round, for every hosted client c (not suppressed):
+
+    1. **publish** — version += 1; encode x_c for the wire into send slot ``version % 2``
+       (``fp32`` or ``bf16`` full snapshot: a lossy mailbox cannot carry an error-feedback delta
+       chain, a receiver may skip versions), hash it on the GPU (SHA-256 Merkle root = the
+       sender's ledger commitment), and **post** it to every destination rank's inbox on side
+       streams — the copies run over xGMI under the next round's training.
+    2. **fetch** — for every remote neighbour, take whatever complete snapshot is newest in its
+       inbox (skip if none is newer than the one held); re-hash and compare with the committed
+       root, keep it only if they match.
+    3. **mix** — x_c <- W_cc x_c + sum_j W_cj view_j with the freshest verified view of each
+       neighbour; a neighbour whose newest snapshot is older than ``liveness_timeout`` rounds
+       (slow, stopped or exited) is treated as dead and its weight folds into c's self-weight.
+
+    ``sync=True`` turns step 2 into a bounded wait: poll until every live neighbour has published
+    round r (or ``sync_timeout_s`` passes and it is declared dead) — lock-step semantics without
+    any matched transfer, for the sync-vs-async comparison.
+    """
+
+    def __init__(self, num_clients: int, states: Dict[int, torch.Tensor], nbrs: Dict[int, List[int]],
+                 wire: str = "bf16", sync: bool = False, liveness_timeout: int = 2,
+                 verify: bool = True, sync_timeout_s: float = 60.0, rank: Optional[int] = None,
+                 world: Optional[int] = None):
+        from .mailbox import MailboxTransport
+        rt = D.runtime()
+        self.rank = rt.rank if rank is None else rank
+        self.world = rt.world if world is None else world
+        self.n = num_clients
+        self.states = states
+        self.local = sorted(states)
+        self.nbrs = nbrs
+        if wire in ("bf16_delta", "bf16"):
+            wire = "bf16"
+        if wire not in ("bf16", "fp32"):
+            raise ValueError(f"mailbox gossip carries full snapshots: wire must be bf16 or fp32, got {wire!r}")
+        self.wire = wire
+        self.async_gossip = not sync
+        self.sync_timeout_s = sync_timeout_s
+        self.verify = verify
+        any_state = next(iter(states.values()))
+        self.numel, self.device = any_state.numel(), any_state.device
+        self.wire_dtype = torch.float32 if wire == "fp32" else torch.bfloat16
+        self.remote_needed = sorted({j for c in self.local for j in nbrs[c]
+                                     if client_rank(j, self.world) != self.rank})
+        send_plan = []
+        for c in self.local:
+            dsts = sorted({client_rank(i, self.world) for i in range(self.n) if c in nbrs[i]}
+                          - {self.rank})
+            send_plan += [(c, r) for r in dsts]
+        self.transport = MailboxTransport(self.numel, self.wire_dtype, self.device,
+                                          self.remote_needed, send_plan, self.rank, self.world)
+        z = lambda: torch.zeros(self.numel, dtype=self.wire_dtype, device=self.device)  # noqa: E731
+        self.send_buf = {c: [z(), z()] for c in self.local}
+        self.replica = {j: z() for j in self.remote_needed}
+        self.stage = {j: z() for j in self.remote_needed}
+        self.liveness_timeout = liveness_timeout
+        self.version = {c: 0 for c in self.local}
+        self.steps = {c: 0 for c in self.local}
+        self.applied = {j: 0 for j in self.remote_needed}     # version held in replica[j]
+        self.replica_round = {j: -1 for j in self.remote_needed}
+        self.suppressed: set = set()
+        self.tamper: set = set()     # fault injection: corrupt these clients' payloads after hashing
+        self.dead: set = set()
+        self.torn = 0
+        self.rejected_msgs = 0
+        self.records: List[dict] = []  # ledger records of this round (published + verified)
+        self._round_local = -1
+
+    # ------------------------------------------------------------------------------------
+    def seed_replicas(self, initial: torch.Tensor):
+        """Every client starts from the identical initial model, so every replica (version 0)
+        starts equal to it: a neighbour that never publishes is mixed as the initial model until
+        the staleness bound retires it."""
+        for j in self.remote_needed:
+            ops.cast_copy_(self.replica[j], initial)
+        for c in self.local:
+            ops.cast_copy_(self.send_buf[c][0], initial)
+            ops.cast_copy_(self.send_buf[c][1], initial)
+
+    def view(self, j: int) -> torch.Tensor:
+        if j in self.states:
+            return self.send_buf[j][self.version[j] % 2]
+        return self.replica[j]
+
+    @torch.no_grad()
+    def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None):
+        from .mailbox import Snapshot
+        roots = {}
+        for c in self.local:
+            if c in self.suppressed:
+                continue
+            self.version[c] += 1
+            self.steps[c] += int((steps or {}).get(c, 0))
+            slot = self.version[c] % 2
+            if self.transport.is_cuda:
+                self.transport.wait_slot_free(c, slot)
+            buf = self.send_buf[c][slot]
+            ops.cast_copy_(buf, self.states[c])
+            roots[c] = ops.merkle_root_deferred(buf) if self.verify else None
+            if c in self.tamper:  # in-flight corruption AFTER the commitment was computed
+                buf.view(-1)[: min(64, buf.numel())].add_(1.0)
+            snap = Snapshot(self.version[c], round_idx, self.steps[c], buf.numel() * buf.element_size(),
+                            b"\0" * 32)
+            rd = roots[c]
+            if rd is not None and not torch.is_tensor(rd):
+                snap.root = bytes(rd)
+                rd = None
+            self.transport.post(c, buf, snap, rd)
+        for c, rd in roots.items():
+            self.records.append({"client": c, "kind": "update", "version": self.version[c],
+                                 "root_t": rd})
+
+    @torch.no_grad()
+    def collect(self, round_idx: int):
+        """Fetch every newer complete snapshot (sync: wait for round ``round_idx``), verify its
+        Merkle root against the sender's commitment, adopt the good ones."""
+        import time as _time
+        want = {j: self.applied[j] for j in self.remote_needed}
+        got = self.transport.fetch(want, self.stage)
+        if not self.async_gossip:
+            t0 = _time.perf_counter()
+            need = {j for j in self.remote_needed if j not in self.dead}
+            have = {j for j, s in got.items() if s.round >= round_idx}
+            while need - have and _time.perf_counter() - t0 < self.sync_timeout_s:
+                _time.sleep(0.0005)
+                more = self.transport.fetch({j: max(self.applied[j], got[j].version if j in got else 0)
+                                             for j in need - have}, self.stage)
+                got.update(more)
+                have |= {j for j, s in more.items() if s.round >= round_idx}
+        self.torn = self.transport.torn
+        ok = {}
+        if got and self.verify:
+            roots = {j: ops.merkle_root_deferred(self.stage[j]) for j in got}
+            for j, rt in roots.items():
+                ok[j] = ops.root_bytes(rt) == got[j].root
+        for j, snap in got.items():
+            good = ok.get(j, True)
+            self.records.append({"client": j, "kind": "recv", "version": snap.version,
+                                 "root": snap.root.hex(), "ok": good, "src_round": snap.round})
+            if not good:
+                self.rejected_msgs += 1
+                continue
+            self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
+            self.applied[j] = snap.version
+            self.replica_round[j] = snap.round
+
+    def _age_out(self, round_idx: int):
+        for j in self.remote_needed:
+            if round_idx - self.replica_round[j] > self.liveness_timeout:
+                self.dead.add(j)
+            else:
+                self.dead.discard(j)
+        for c in self.local:  # a suppressed (dead) local client stops being fresh too
+            if c in self.suppressed and round_idx > self.liveness_timeout:
+                self.dead.add(c)
+
+    def live_matrix(self, W: np.ndarray) -> np.ndarray:
+        return GossipEngine.live_matrix(self, W)
+
+    @torch.no_grad()
+    def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None):
+        return GossipEngine.mix(self, W, param_out)
+
+    def end_of_round(self, round_idx: int, W: np.ndarray,
+                     param_out: Optional[Dict[int, torch.Tensor]] = None,
+                     steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
+        self.records = []
+        b0 = self.transport.bytes_posted
+        self.publish(round_idx, steps)
+        self.collect(round_idx)
+        self._age_out(round_idx)
+        self.mix(self.live_matrix(W), param_out)
+        ages = [round_idx - self.replica_round[j] for j in self.remote_needed if j not in self.dead]
+        return {"mixed": 1.0, "stale_rounds": float(np.mean(ages)) if ages else 0.0,
+                "bytes_sent": float(self.transport.bytes_posted - b0),
+                "dead_peers": float(len(self.dead)), "torn": float(self.torn),
+                "rejected_msgs": float(self.rejected_msgs)}
+
+    def drain(self):
+        self.transport.drain()
+
+    def close(self):
+        self.transport.close()

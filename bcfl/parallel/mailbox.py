@@ -1,0 +1,284 @@
+"""One-sided peer mailboxes: truly asynchronous P2P gossip.
+
+The paper's claim is *asynchronous* peer-to-peer exchange — a node's information-passing time is
+the max over destinations, not the sum (``README.md:10``; ``Medical_Transcriptions_All_graphs.ipynb:
+979-980``). RCCL send/recv cannot give that: every send needs a matching receive, so one slow or
+dead peer stalls its neighbours. Here nothing is ever matched:
+
+* every rank owns an **inbox** per remote client it listens to: a header region (2 slots x 16
+  int64 words) and a payload region (2 slots of the wire-encoded model);
+* inboxes are exported ONCE (``hipIpcGetMemHandle``; on CPU a ``/dev/shm`` file) and the handles
+  all-gathered at start-up; each sender maps the inboxes of its destinations;
+* **post** (sender, side HIP stream): for version v into slot v % 2 — header.begin = v, payload
+  copy over xGMI (``hipMemcpyAsync`` into the peer's memory), header body (round, steps, bytes,
+  SHA-256 Merkle root of the payload) and, fenced after it, header.end = v;
+* **fetch** (receiver, any time): read both slot headers, take the newest slot with
+  begin == end, copy its payload into a local replica, re-read the header — if begin moved, the
+  sender lapped the slot mid-copy and the snapshot is dropped (seqlock). A peer that is slow,
+  stopped, or gone simply leaves the last good snapshot in place; the gossip layer ages it out
+  (staleness bound) instead of waiting.
+
+The header's Merkle root is the sender's ledger commitment: the receiver re-hashes the fetched
+payload on its GPU and rejects a snapshot whose root does not match (tampering in flight).
+
+Backends: ``HipIpcBackend`` (GPU tensors; uncached device memory, peer-mapped) and ``ShmBackend``
+(CPU tensors in shared-memory files, the CPU-test analogue with the identical protocol).
+"""
+from __future__ import annotations
+
+import os
+import uuid
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import dist as D
+
+HDR_WORDS = 16
+W_BEGIN, W_ROUND, W_STEPS, W_BYTES, W_ROOT, W_END = 0, 1, 2, 3, 4, 8
+ALIGN = 4096
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def root_to_words(root: bytes) -> List[int]:
+    """32-byte SHA-256 root -> 4 signed int64 header words."""
+    return [int(x) for x in np.frombuffer(root, dtype="<i8")]
+
+
+def words_to_root(words: Sequence[int]) -> bytes:
+    return np.asarray(list(words), dtype="<i8").tobytes()
+
+
+@dataclass
+class Snapshot:
+    version: int
+    round: int
+    steps: int
+    nbytes: int
+    root: bytes
+
+
+# ----------------------------------------------------------------------------------------------
+class ShmBackend:
+    """CPU analogue: regions are files under /dev/shm mapped with ``torch.from_file(shared=True)``;
+    a handle is the file path. Writes are plain stores (x86 keeps store order)."""
+
+    def __init__(self, tag: str):
+        self.tag = tag
+        self.owned: List[str] = []
+        self.root = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+
+    def alloc(self, nbytes: int, kind: str) -> Tuple[torch.Tensor, object]:
+        path = os.path.join(self.root, f"bcfl_mbox_{self.tag}_{uuid.uuid4().hex[:12]}_{kind}")
+        with open(path, "wb") as fh:
+            fh.truncate(nbytes)
+        self.owned.append(path)
+        return torch.from_file(path, shared=True, size=nbytes, dtype=torch.uint8), path
+
+    def open(self, handle, nbytes: int) -> torch.Tensor:
+        return torch.from_file(handle, shared=True, size=nbytes, dtype=torch.uint8)
+
+    def hdr_store(self, hdr: torch.Tensor, slot: int, words: Sequence[int], off: int,
+                  end_word: int = -1, end_value: int = 0):
+        row = hdr[slot]
+        if words:
+            row[off:off + len(words)] = torch.tensor(list(words), dtype=torch.int64)
+        if end_word >= 0:
+            row[end_word] = int(end_value)
+
+    def release_names(self):
+        for p in self.owned:
+            try:
+                os.remove(p)
+            except FileNotFoundError:
+                pass
+        self.owned.clear()
+
+    close = release_names
+
+
+class HipIpcBackend:
+    """GPU: dedicated uncached device allocations exported with hipIpcGetMemHandle, mapped by
+    peers with hipIpcOpenMemHandle (xGMI peer access); header stores are a fenced kernel."""
+
+    def __init__(self, device: torch.device):
+        from .. import ops
+        self.C = ops.native()
+        self.device = device
+
+    def alloc(self, nbytes: int, kind: str) -> Tuple[torch.Tensor, object]:
+        t = self.C.mbox_alloc(int(nbytes), int(self.device.index), 3)
+        return t, bytes(self.C.ipc_handle(t))
+
+    def open(self, handle, nbytes: int) -> torch.Tensor:
+        return self.C.ipc_open(handle, int(nbytes), int(self.device.index))
+
+    def hdr_store(self, hdr: torch.Tensor, slot: int, words: Sequence[int], off: int,
+                  end_word: int = -1, end_value: int = 0):
+        self.C.hdr_store(hdr.view(-1), int(slot), [int(w) for w in words], int(off), int(end_word),
+                         int(end_value))
+
+    def release_names(self):
+        pass
+
+    def close(self):
+        pass
+
+
+# ----------------------------------------------------------------------------------------------
+class _Box:
+    """Views of one inbox (local or a peer's mapped copy)."""
+
+    def __init__(self, hdr_raw: torch.Tensor, pay_raw: torch.Tensor, numel: int, dtype: torch.dtype):
+        self.hdr = hdr_raw[: 2 * HDR_WORDS * 8].view(torch.int64).view(2, HDR_WORDS)
+        esz = torch.tensor([], dtype=dtype).element_size()
+        ps = _align(numel * esz)
+        self.slots = [pay_raw[k * ps:k * ps + numel * esz].view(dtype) for k in (0, 1)]
+        self._keep = (hdr_raw, pay_raw)
+
+
+class MailboxTransport:
+    """Inboxes for ``listen`` (remote clients this rank reads) and mapped peer inboxes for
+    ``send_plan`` ((local client, destination rank) pairs). Construction is collective (one
+    all-gather of handles); everything after it is one-sided."""
+
+    def __init__(self, numel: int, dtype: torch.dtype, device: torch.device, listen: Sequence[int],
+                 send_plan: Sequence[Tuple[int, int]], rank: Optional[int] = None,
+                 world: Optional[int] = None):
+        rt = D.runtime()
+        self.rank = rt.rank if rank is None else rank
+        self.world = rt.world if world is None else world
+        self.numel, self.dtype, self.device = numel, dtype, device
+        self.is_cuda = device.type == "cuda"
+        esz = torch.tensor([], dtype=dtype).element_size()
+        self.payload_bytes = numel * esz
+        self.hdr_bytes = ALIGN
+        self.pay_bytes = 2 * _align(self.payload_bytes)
+        self.backend = HipIpcBackend(device) if self.is_cuda else ShmBackend(f"r{self.rank}")
+        self.inbox: Dict[int, _Box] = {}
+        handles = {}
+        for j in listen:
+            h, hh = self.backend.alloc(self.hdr_bytes, f"h{j}")
+            p, ph = self.backend.alloc(self.pay_bytes, f"p{j}")
+            self.inbox[j] = _Box(h, p, numel, dtype)
+            handles[j] = (hh, ph)
+        table = D.all_gather_object(handles)  # the only collective: handle exchange at start-up
+        self.outbox: Dict[int, List[Tuple[int, _Box]]] = {}
+        for c, dst in send_plan:
+            hh, ph = table[dst][c]
+            box = _Box(self.backend.open(hh, self.hdr_bytes), self.backend.open(ph, self.pay_bytes),
+                       numel, dtype)
+            self.outbox.setdefault(c, []).append((dst, box))
+        self.streams = ({d: torch.cuda.Stream(device=device) for d in {d for _, d in send_plan}}
+                        if self.is_cuda else {})
+        # every peer has mapped its destinations: shared-memory names can go now (mappings stay
+        # valid), so nothing is left in /dev/shm even if a rank dies without closing
+        D.barrier()
+        self.backend.release_names()
+        self.posted: Dict[Tuple[int, int], List["torch.cuda.Event"]] = {}  # (client, slot)
+        self.torn = 0
+        self.bytes_posted = 0
+
+    # ------------------------------------------------------------------ sender
+    def wait_slot_free(self, c: int, slot: int):
+        """Make the current stream wait until the earlier posts that READ client c's send buffer
+        ``slot`` have finished (the caller is about to overwrite it)."""
+        for ev in self.posted.pop((c, slot), []):
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def post(self, c: int, payload: torch.Tensor, snap: Snapshot,
+             root_dev: Optional[torch.Tensor] = None):
+        """Publish ``payload`` (wire-encoded, ``numel`` elements) as version ``snap.version`` of
+        client c to every destination inbox. Returns immediately on GPU (side streams).
+
+        ``root_dev``: the payload's Merkle root as a 32-byte device tensor, copied device-to-device
+        into the header (no host round trip); otherwise ``snap.root`` (host bytes) is written."""
+        slot = snap.version % 2
+        body = [snap.round, snap.steps, snap.nbytes]
+        if root_dev is None:
+            body += root_to_words(snap.root)
+        evs = []
+        if self.is_cuda:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.device))
+        for dst, box in self.outbox.get(c, []):
+            if self.is_cuda:
+                st = self.streams[dst]
+                st.wait_event(ready)
+                with torch.cuda.stream(st):
+                    self.backend.hdr_store(box.hdr, slot, [snap.version], W_BEGIN)
+                    box.slots[slot].copy_(payload, non_blocking=True)
+                    if root_dev is not None:
+                        box.hdr[slot, W_ROOT:W_ROOT + 4].copy_(root_dev.view(torch.int64),
+                                                               non_blocking=True)
+                    self.backend.hdr_store(box.hdr, slot, body, W_ROUND, W_END, snap.version)
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    evs.append(ev)
+            else:
+                self.backend.hdr_store(box.hdr, slot, [snap.version], W_BEGIN)
+                box.slots[slot].copy_(payload)
+                if root_dev is not None:
+                    box.hdr[slot, W_ROOT:W_ROOT + 4] = root_dev.view(torch.int64)
+                self.backend.hdr_store(box.hdr, slot, body, W_ROUND, W_END, snap.version)
+            self.bytes_posted += self.payload_bytes
+        if evs:
+            self.posted[(c, slot)] = evs
+
+    def drain(self):
+        for evs in self.posted.values():
+            for ev in evs:
+                ev.synchronize()
+        self.posted.clear()
+
+    # ------------------------------------------------------------------ receiver
+    def headers(self, js: Sequence[int]) -> Dict[int, np.ndarray]:
+        """Both slot headers of every inbox in ``js`` (one device->host read)."""
+        if not js:
+            return {}
+        h = torch.stack([self.inbox[j].hdr for j in js]).cpu().numpy()
+        return {j: h[i] for i, j in enumerate(js)}
+
+    @staticmethod
+    def newest(h: np.ndarray) -> Optional[Tuple[int, Snapshot]]:
+        best = None
+        for s in (0, 1):
+            v = int(h[s, W_BEGIN])
+            if v > 0 and v == int(h[s, W_END]) and (best is None or v > best[1].version):
+                best = (s, Snapshot(v, int(h[s, W_ROUND]), int(h[s, W_STEPS]), int(h[s, W_BYTES]),
+                                    words_to_root(h[s, W_ROOT:W_ROOT + 4])))
+        return best
+
+    def fetch(self, want: Dict[int, int], out: Dict[int, torch.Tensor]) -> Dict[int, Snapshot]:
+        """For every inbox j with a complete version newer than ``want[j]``, copy it into
+        ``out[j]`` (stream-ordered) and return the validated snapshots; torn reads are dropped."""
+        js = list(want)
+        first = self.headers(js)
+        picked: Dict[int, Tuple[int, Snapshot]] = {}
+        for j in js:
+            nw = self.newest(first[j])
+            if nw is not None and nw[1].version > want[j]:
+                picked[j] = nw
+                out[j].copy_(self.inbox[j].slots[nw[0]], non_blocking=self.is_cuda)
+        if not picked:
+            return {}
+        second = self.headers(list(picked))  # stream-ordered after the payload copies
+        good = {}
+        for j, (slot, snap) in picked.items():
+            h = second[j]
+            if int(h[slot, W_BEGIN]) == snap.version and int(h[slot, W_END]) == snap.version:
+                good[j] = snap
+            else:
+                self.torn += 1
+        return good
+
+    def close(self):
+        self.drain()
+        self.outbox.clear()
+        self.inbox.clear()
+        self.backend.close()

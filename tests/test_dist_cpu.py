@@ -90,7 +90,7 @@ def test_serverless_bf16_delta_wire_close(tmp_path):
 
 
 def test_serverless_async_runs_and_mixes(tmp_path):
-    kw = {"async_gossip": True, "num_rounds": 3, "anomaly_filter": "both"}
+    kw = {"async_gossip": True, "num_rounds": 3, "anomaly_filter": "both", "gossip_transport": "rccl"}
     res = run_world(_fed_worker, 2, str(tmp_path / "d"), "serverless", str(tmp_path / "d"), kw)
     a, b = res[0]["master"], res[1]["master"]
     assert torch.isfinite(a).all() and torch.isfinite(b).all()
@@ -169,7 +169,7 @@ def _torn_worker(rank, world):
     eng.seed_replicas(torch.zeros(64))
     eng.publish(0)
     if rank == 1:  # tear the message: head / tail versions differ
-        eng.send_hdr[1][3] += 1
+        eng.send_hdr[1][7] += 1
     eng.launch(0)
     eng.finish()
     return {"torn": torch.tensor(eng.torn), "replica": eng.replica[1 - rank].clone()}

@@ -1,0 +1,138 @@
+"""One-sided mailbox gossip (bcfl.parallel.mailbox): the CPU analogue (shared-memory inboxes,
+gloo for the one start-up handle exchange) of the hipIpc transport. Properties: posts need no
+matching receive, torn snapshots are rejected, tampered payloads fail the Merkle commitment and are
+recorded in the ledger, and a slow or EXITED peer never stalls the others."""
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_world
+
+
+def _cfg(out, **kw):
+    from bcfl.config import FLConfig
+    base = dict(mode="serverless", model="tiny-bert", dataset="tiny", num_clients=2, num_rounds=3,
+                train_samples=48, test_samples=16, global_test_samples=32, batch_size=16, lr=1e-3,
+                out_dir=out, partition="label_shards", reference_prints=False, save_every=0,
+                device="cpu", backend="gloo", async_gossip=True, gossip_transport="mailbox")
+    base.update(kw)
+    return FLConfig(**base)
+
+
+def _transport_worker(rank, world):
+    from bcfl.parallel import dist as D
+    from bcfl.parallel.mailbox import MailboxTransport, Snapshot
+    D.init_runtime("cpu", "gloo")
+    peer = 1 - rank
+    tr = MailboxTransport(1000, torch.float32, torch.device("cpu"), listen=[peer],
+                          send_plan=[(rank, peer)])
+    try:
+        D.barrier()
+        x = torch.arange(1000, dtype=torch.float32) + 1000 * rank
+        tr.post(rank, x, Snapshot(1, 0, 8, 4000, bytes(range(32))))
+        D.barrier()  # only so the test knows the post landed; the protocol never waits
+        out = {peer: torch.zeros(1000)}
+        got = tr.fetch({peer: 0}, out)
+        again = tr.fetch({peer: 1}, out)  # nothing newer than version 1
+        # a half-written version: begin = 3 without end -> the reader keeps version 1
+        tr.backend.hdr_store(tr.outbox[rank][0][1].hdr, 1, [3], 0)
+        D.barrier()
+        torn_view = tr.fetch({peer: 1}, out)
+        return {"data": out[peer].clone(), "version": torch.tensor(got[peer].version),
+                "root_ok": torch.tensor(got[peer].root == bytes(range(32))),
+                "again": torch.tensor(len(again)), "half": torch.tensor(len(torn_view))}
+    finally:
+        D.barrier()
+        tr.close()
+
+
+def test_mailbox_transport_post_fetch(tmp_path):
+    res = run_world(_transport_worker, 2, str(tmp_path))
+    assert torch.equal(res[0]["data"], torch.arange(1000, dtype=torch.float32) + 1000)
+    assert torch.equal(res[1]["data"], torch.arange(1000, dtype=torch.float32))
+    for r in res:
+        assert int(r["version"]) == 1 and bool(r["root_ok"])
+        assert int(r["again"]) == 0 and int(r["half"]) == 0
+
+
+def _fed_worker(rank, world, out, kw, stop_after=None):
+    from bcfl.fl import Federation
+    fed = Federation(_cfg(out, **kw), verbose=False)
+    times = []
+    for r in range(fed.cfg.num_rounds):
+        if stop_after is not None and rank == 1 and r == stop_after:
+            return {"exited": torch.tensor(1)}  # this rank leaves for good, mid-run
+        t0 = time.perf_counter()
+        fed.run_round(r)
+        times.append(time.perf_counter() - t0)
+    fed.finish(audit=stop_after is None)
+    blocks = fed.ledger.blocks() if fed.ledger is not None else []
+    return {"master": fed.flat.master.clone(), "times": torch.tensor(times),
+            "dead": torch.tensor(sorted(fed.gossip.dead), dtype=torch.int64),
+            "rejects": torch.tensor(sum(b["kind"] == "verify" and b["verdict"] == "reject"
+                                        for b in blocks)),
+            "accepts": torch.tensor(sum(b["kind"] == "verify" and b["verdict"] == "accept"
+                                        for b in blocks)),
+            "acc": torch.tensor([h["global_acc"] for h in fed.history]),
+            "audit": torch.tensor(-1 if fed.ledger_audit is None else fed.ledger_audit["mismatched"])}
+
+
+def test_mailbox_federation_async_runs(tmp_path):
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), {})
+    for r in res:
+        assert torch.isfinite(r["master"]).all()
+        assert int(r["accepts"]) >= 1 and int(r["rejects"]) == 0
+        assert int(r["audit"]) == 0  # every accepted update matches its sender's commitment
+    assert os.path.exists(tmp_path / "d" / "ledger.jsonl")
+    assert os.path.exists(tmp_path / "d" / "ledger.rank1.jsonl")
+
+
+def test_mailbox_sync_equals_single_process(tmp_path):
+    """Sync mailbox + fp32 wire: every round mixes the fresh snapshots, exactly like one process
+    hosting both clients."""
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    kw = {"async_gossip": False, "wire_dtype": "fp32"}
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), kw)
+    D.set_runtime_for_tests(None)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(2)
+    try:
+        fed = Federation(_cfg(str(tmp_path / "s"), **kw), verbose=False)
+        fed.run()
+    finally:
+        torch.set_num_threads(nt)
+        D.set_runtime_for_tests(None)
+    assert torch.equal(res[0]["master"], res[1]["master"])
+    assert torch.equal(res[0]["master"], fed.flat.master)
+
+
+def test_mailbox_tamper_rejected_and_logged(tmp_path):
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"inject_tamper": [1], "num_rounds": 3})
+    # rank 0 rejects every (corrupted) update of client 1; rank 1 accepts client 0's
+    assert int(res[0]["rejects"]) >= 1 and int(res[0]["accepts"]) == 0
+    assert int(res[1]["rejects"]) == 0 and int(res[1]["accepts"]) >= 1
+    assert 1 in res[0]["dead"].tolist()  # never a good snapshot -> aged out of the mix
+    rows = [l for l in open(tmp_path / "d" / "ledger.jsonl") if '"verify"' in l]
+    assert rows and all('"reject"' in l and "merkle root mismatch" in l for l in rows)
+
+
+def test_mailbox_slow_peer_does_not_stall(tmp_path):
+    # client 1 (rank 1) sleeps 5 s per round; rank 0 keeps its own pace
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"inject_slow": {1: 5000.0}, "num_rounds": 3})
+    assert float(res[1]["times"].min()) >= 5.0
+    assert float(res[0]["times"].max()) < 4.0
+
+
+def test_mailbox_exited_peer_does_not_stall(tmp_path):
+    # rank 1 leaves after round 1; rank 0 completes every round and ages client 1 out
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"num_rounds": 6, "liveness_timeout": 1}, 1)
+    assert int(res[1]["exited"]) == 1
+    assert len(res[0]["times"]) == 6
+    assert res[0]["dead"].tolist() == [1]
