@@ -96,6 +96,12 @@ def dir_size_gb(path: str) -> float:
 
 
 class AsyncCheckpointer:
+    """HF-layout checkpoints written off the critical path: each job's fp32 master is copied
+    device->pinned host on a copy stream, then a writer thread serialises it. The compute stream
+    waits (on the GPU, no host sync) for the copies before anything can overwrite a source buffer,
+    so a checkpoint never mixes two rounds' weights. A save requested while the previous write is
+    still running is skipped and counted (``skipped``)."""
+
     def __init__(self, model, flat, async_: bool = True):
         self.model, self.flat = model, flat
         self.layout = hf_layout(model, flat)
@@ -103,7 +109,7 @@ class AsyncCheckpointer:
         self.async_ = async_
         dev = flat.master.device
         self.cuda = dev.type == "cuda"
-        self.pinned = torch.empty(flat.numel, dtype=torch.float32, pin_memory=self.cuda)
+        self.pinned: List[torch.Tensor] = []
         self.stream = torch.cuda.Stream(device=dev) if self.cuda else None
         self.pool = cf.ThreadPoolExecutor(max_workers=1) if async_ else None
         self.future: Optional[cf.Future] = None
@@ -115,34 +121,55 @@ class AsyncCheckpointer:
     def busy(self) -> bool:
         return self.future is not None and not self.future.done()
 
+    def _buf(self, i: int) -> torch.Tensor:
+        while len(self.pinned) <= i:
+            self.pinned.append(torch.empty(self.flat.numel, dtype=torch.float32,
+                                           pin_memory=self.cuda))
+        return self.pinned[i]
+
     def save(self, out_dirs: List[str], master: Optional[torch.Tensor] = None,
-             metadata: Optional[Dict[str, str]] = None, state: Optional[Dict[str, Any]] = None) -> bool:
+             metadata: Optional[Dict[str, str]] = None, state: Optional[Dict[str, Any]] = None,
+             jobs: Optional[List[tuple]] = None, extra_files: Optional[Dict[str, Any]] = None) -> bool:
+        """``jobs``: [(dirs, fp32 flat master)] (default: one job ``(out_dirs, master)``);
+        ``state`` is written as ``state.json`` into the first job's dirs; ``extra_files``:
+        {path: torch-serialisable object} written by the same thread (resume state)."""
         if self.busy():
             self.skipped += 1
             return False
-        src = self.flat.master if master is None else master
+        if jobs is None:
+            jobs = [(out_dirs, self.flat.master if master is None else master)]
+        bufs = [self._buf(i) for i in range(len(jobs))]
         if self.cuda:
-            ev = torch.cuda.current_stream(src.device).record_event()
+            cur = torch.cuda.current_stream(self.stream.device)
+            ev = cur.record_event()
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
-                self.pinned.copy_(src, non_blocking=True)
+                for b, (_, src) in zip(bufs, jobs):
+                    b.copy_(src, non_blocking=True)
                 done = self.stream.record_event()
+            cur.wait_event(done)  # later writers of the sources are ordered after the copies
         else:
-            self.pinned.copy_(src)
+            for b, (_, src) in zip(bufs, jobs):
+                b.copy_(src)
             done = None
 
         def _write():
             if done is not None:
                 done.synchronize()
-            host = self.pinned.numpy()
-            for d in out_dirs:
-                save_dir(d, self.model, host, self.layout, self.config, metadata)
-                if state is not None:
-                    with open(os.path.join(d, "state.json"), "w") as fh:
-                        json.dump(state, fh, indent=2, sort_keys=True, default=str)
+            for k, (b, (dirs, _)) in enumerate(zip(bufs, jobs)):
+                host = b.numpy()
+                for d in dirs:
+                    save_dir(d, self.model, host, self.layout, self.config, metadata)
+                    if state is not None and k == 0:
+                        with open(os.path.join(d, "state.json"), "w") as fh:
+                            json.dump(state, fh, indent=2, sort_keys=True, default=str)
+            for path, obj in (extra_files or {}).items():
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                torch.save(obj, path + ".tmp")
+                os.replace(path + ".tmp", path)
             with self._lock:
                 self.saved += 1
-                self.last_dir = out_dirs[0] if out_dirs else None
+                self.last_dir = jobs[0][0][0] if jobs and jobs[0][0] else None
 
         if self.async_:
             self.future = self.pool.submit(_write)

@@ -82,7 +82,8 @@ class FLConfig:
     # --- io / observability -----------------------------------------------------------
     out_dir: str = "runs/default"
     save_every: int = 1
-    save_clients: bool = False
+    save_clients: bool = False          # also <out>/client_{k}/ for every hosted client
+    save_resume_state: bool = False     # also <out>/resume/rank{r}.pt (clients, optimizer, RNG, gossip)
     compat_save_path: Optional[str] = None   # e.g. "my_albert_model2"
     async_ckpt: bool = True
     resume: Optional[str] = None

@@ -190,6 +190,7 @@ class Federation:
         self.ledger = Ledger(genesis={"model": cfg.model, "mode": cfg.mode, "clients": n,
                                       "dataset": cfg.dataset, "partition": cfg.partition},
                              path=self._ledger_path() if cfg.ledger else None,
+                             truncate=not cfg.resume,
                              ts=0.0) if cfg.ledger else None
         # ---------------- io ---------------------------------------------------------------------------
         self.metrics = MetricsWriter(os.path.join(out, "metrics.jsonl"),
@@ -741,14 +742,14 @@ class Federation:
         self._log_provenance(r)
         t0 = time.perf_counter()
         res = self.server_round(r) if self.cfg.mode == "server" else self.serverless_round(r)
-        self._maybe_save(r)
-        t_round = time.perf_counter() - t0
         ge: Optional[EvalResult] = res.get("global")
         gacc = ge.accuracy if ge is not None else None
         if gacc is not None:
             self.global_accuracies.append(gacc)
-            if self.verbose and self.cfg.reference_prints:
-                print(f"Global Model Accuracy: {gacc * 100:.2f}%", flush=True)
+        self._maybe_save(r)
+        t_round = time.perf_counter() - t0
+        if gacc is not None and self.verbose and self.cfg.reference_prints:
+            print(f"Global Model Accuracy: {gacc * 100:.2f}%", flush=True)
         rec = {"round": r, "mode": self.cfg.mode, "t_round": t_round, "global_acc": gacc,
                "global_majority_rate": self.global_majority_rate(r) if gacc is not None else None,
                "global_eval_rows": int(ge.count) if ge is not None else 0,
@@ -770,20 +771,52 @@ class Federation:
         return rec
 
     def _maybe_save(self, r: int):
+        """Reference C16 (``save_pretrained`` every round, ``serverless_NonIID_IMDB.py:305``):
+        ``<out>/global`` (rank 0), ``<out>/client_{k}`` for EVERY hosted client with
+        ``save_clients``, and with ``save_resume_state`` the per-rank state a resumed run needs to
+        continue bit-identically (``<out>/resume/rank{r}.pt``)."""
         cfg = self.cfg
         if self.ckpt is None or (r + 1) % cfg.save_every:
             return
         with self.timer.phase("ckpt"):
             state = {"round": r, "rng": ops.rng.global_rng().state(),
                      "ledger_tip": self.ledger.tip if self.ledger else None,
+                     "ledger_height": len(self.ledger) if self.ledger else 0,
                      "global_accuracies": self.global_accuracies, "config": cfg.to_dict()}
-            dirs = []
+            jobs = []
             if self.rt.is_main:
-                dirs.append(os.path.join(cfg.out_dir, "global"))
-            if cfg.save_clients and self.local_clients:
-                dirs.append(os.path.join(cfg.out_dir, f"client_{self.local_clients[0]}"))
-            src = self.global_master if cfg.mode == "server" else self.flat.master
-            self.ckpt.save(dirs, master=src, metadata={"round": str(r)}, state=state)
+                src = self.global_master if cfg.mode == "server" else self.flat.master
+                jobs.append(([os.path.join(cfg.out_dir, "global")], src))
+            if cfg.save_clients:
+                for c in self.local_clients:
+                    src = self.client_master.get(c, self.flat.master)
+                    jobs.append(([os.path.join(cfg.out_dir, f"client_{c}")], src))
+            extra = None
+            if cfg.save_resume_state:
+                extra = {os.path.join(cfg.out_dir, "resume", f"rank{self.rt.rank}.pt"):
+                         self.resume_state(r)}
+            if jobs or extra:
+                self.ckpt.save([], metadata={"round": str(r)},
+                               state=state if self.rt.is_main else None, jobs=jobs,
+                               extra_files=extra)
+
+    def resume_state(self, r: int) -> dict:
+        """Per-rank training state (tensors on the host; loadable with ``weights_only=True``)."""
+        cpu = lambda t: t.detach().cpu().clone()  # noqa: E731
+        st = {"round": int(r), "rank": self.rt.rank, "world": self.rt.world,
+              "rng": ops.rng.global_rng().state(),
+              "client_rng": {int(c): dict(v) for c, v in self.client_rng.items()},
+              "client_master": {int(c): cpu(t) for c, t in self.client_master.items()},
+              "master": cpu(self.flat.master),
+              "client_opt": {int(c): {"m": cpu(o["m"]), "v": cpu(o["v"]), "step": int(o["step"])}
+                             for c, o in self.client_opt.items()},
+              "prev_rejected": sorted(self.prev_verdicts.rejected),
+              "tokens_trained": int(self.tokens_trained)}
+        if self.global_master is not None:
+            st["global_master"] = cpu(self.global_master)
+        if self.gossip is not None and hasattr(self.gossip, "state_dict"):
+            st["gossip"] = self.gossip.state_dict()
+        return st
 
     def run(self, rounds: Optional[int] = None) -> List[dict]:
         cfg = self.cfg
@@ -870,10 +903,38 @@ class Federation:
             self.gossip.seed_replicas(self.flat.master)
         self.start_round = int(st["round"]) + 1
         self.global_accuracies = list(st.get("global_accuracies", []))
+        rs = os.path.join(path, "resume", f"rank{self.rt.rank}.pt")
+        if os.path.exists(rs):
+            self._load_resume_state(torch.load(rs, weights_only=True, map_location="cpu"))
         led = os.path.join(path, "ledger.jsonl")
         if self.ledger is not None and os.path.exists(led):
             old = Ledger.load(led)
             if old.verify() != -1:
                 raise RuntimeError("ledger in resume dir fails verification")
+            if st.get("ledger_height") and len(old) > int(st["ledger_height"]):
+                old = old.truncated(int(st["ledger_height"]))  # blocks after the checkpoint
+            if st.get("ledger_tip") and old.tip != st["ledger_tip"]:
+                raise RuntimeError("ledger tip does not match the checkpoint's ledger_tip")
             self.ledger = old
-            self.ledger.path = led if self.rt.is_main else None
+            self.ledger.path = self._ledger_path()  # continue the chain in this run's out_dir
+            self.ledger.rewrite()
+
+    @torch.no_grad()
+    def _load_resume_state(self, st: dict):
+        if int(st["world"]) != self.rt.world:
+            raise ValueError(f"resume state is for world {st['world']}, this run has {self.rt.world}")
+        ops.rng.global_rng().load_state(st["rng"])
+        for c, v in st["client_rng"].items():
+            self.client_rng[int(c)] = dict(v)
+        for c, t in st["client_master"].items():
+            self.client_master[int(c)].copy_(t)
+        self.flat.load_master(st["master"].to(self.device))
+        for c, o in st["client_opt"].items():
+            self.client_opt[int(c)] = {"m": o["m"].to(self.device), "v": o["v"].to(self.device),
+                                       "step": int(o["step"])}
+        if self.global_master is not None and "global_master" in st:
+            self.global_master.copy_(st["global_master"])
+        self.prev_verdicts = Verdicts(rejected=set(int(x) for x in st.get("prev_rejected", [])))
+        self.tokens_trained = int(st.get("tokens_trained", 0))
+        if self.gossip is not None and "gossip" in st:
+            self.gossip.load_state_dict(st["gossip"])

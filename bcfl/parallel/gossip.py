@@ -78,6 +78,7 @@ class GossipEngine:
             self._replicas_seeded = False
         self.pending: Optional[D.P2PHandle] = None
         self.pending_round: Optional[int] = None
+        self.ready = False
         self.bytes_sent_last = 0
         # versions / liveness (host bookkeeping + tiny device headers) ---------------------------
         self.liveness_timeout = liveness_timeout
@@ -157,6 +158,7 @@ class GossipEngine:
             return False
         self.pending.wait()
         self.pending = None
+        self.ready = True  # received, not yet mixed (end_of_round mixes it)
         rnd = self.pending_round if self.pending_round is not None else 0
         hdrs = (torch.stack([self.recv_hdr[j] for j in self.remote_needed]).cpu().tolist()
                 if self.remote_needed else [])
@@ -233,13 +235,15 @@ class GossipEngine:
             self.publish(round_idx, steps)
             self.launch(round_idx)
             self.finish()
+            self.ready = False
             self.mix(self.live_matrix(W), param_out)
             info["mixed"] = 1.0
         else:
-            had = self.pending is not None
+            had = self.pending is not None or self.ready
             if had:
                 src_round = self.pending_round
                 self.finish()
+                self.ready = False
                 self.mix(self.live_matrix(W), param_out)
                 info.update(mixed=1.0, stale_rounds=float(round_idx - src_round))
             self.publish(round_idx, steps)
@@ -255,6 +259,41 @@ class GossipEngine:
 
     def close(self):
         self.drain()
+
+    # ------------------------------------------------------------------------------------
+    def state_dict(self) -> dict:
+        """Everything a resumed run needs to continue bit-identically: wire snapshots / error-
+        feedback references, replicas, versions and liveness bookkeeping. In-flight transfers
+        are completed first (their data is part of the state)."""
+        self.finish()
+        t = lambda d: {int(k): v.detach().cpu().clone() for k, v in d.items()}  # noqa: E731
+        st = {"send_buf": t(self.send_buf), "recv_buf": t(self.recv_buf),
+              "send_hdr": t(self.send_hdr), "recv_hdr": t(self.recv_hdr),
+              "version": dict(self.version), "steps": dict(self.steps),
+              "applied": dict(self.applied), "seen_version": dict(self.seen_version),
+              "fresh_round": dict(self.fresh_round), "dead": sorted(self.dead),
+              "torn": self.torn, "ready": bool(self.ready),
+              "pending_round": -1 if self.pending_round is None else int(self.pending_round)}
+        if self.wire == "bf16_delta":
+            st["ref"], st["replica"] = t(self.ref), t(self.replica)
+        return st
+
+    def load_state_dict(self, st: dict):
+        def put(dst, src):
+            for k, v in src.items():
+                dst[int(k)].copy_(v.to(dst[int(k)].device))
+        for name in ("send_buf", "recv_buf", "send_hdr", "recv_hdr"):
+            put(getattr(self, name), st[name])
+        if self.wire == "bf16_delta":
+            put(self.ref, st["ref"])
+            put(self.replica, st["replica"])
+        for name in ("version", "steps", "applied", "seen_version", "fresh_round"):
+            getattr(self, name).update({int(k): int(v) for k, v in st[name].items()})
+        self.dead = set(int(x) for x in st["dead"])
+        self.torn = int(st["torn"])
+        self.ready = bool(st["ready"])
+        self.pending = None
+        self.pending_round = None if int(st["pending_round"]) < 0 else int(st["pending_round"])
 
 
 @torch.no_grad()
@@ -451,3 +490,24 @@ class MailboxGossip:
 
     def close(self):
         self.transport.close()
+
+    def state_dict(self) -> dict:
+        """Published snapshots, verified replicas, versions and liveness. Inbox contents are NOT
+        state: after a restart peers simply post again (a replica's version tells what is new)."""
+        self.drain()
+        t = lambda d: {int(k): v.detach().cpu().clone() for k, v in d.items()}  # noqa: E731
+        return {"send_buf": {int(c): [b.detach().cpu().clone() for b in v] for c, v in self.send_buf.items()},
+                "replica": t(self.replica), "version": dict(self.version), "steps": dict(self.steps),
+                "applied": dict(self.applied), "replica_round": dict(self.replica_round),
+                "dead": sorted(self.dead), "rejected_msgs": self.rejected_msgs}
+
+    def load_state_dict(self, st: dict):
+        for c, bufs in st["send_buf"].items():
+            for dst, src in zip(self.send_buf[int(c)], bufs):
+                dst.copy_(src.to(dst.device))
+        for j, v in st["replica"].items():
+            self.replica[int(j)].copy_(v.to(self.replica[int(j)].device))
+        for name in ("version", "steps", "applied", "replica_round"):
+            getattr(self, name).update({int(k): int(v) for k, v in st[name].items()})
+        self.dead = set(int(x) for x in st["dead"])
+        self.rejected_msgs = int(st["rejected_msgs"])

@@ -132,7 +132,9 @@ class Ledger:
         self._flushed = len(self)
 
     @classmethod
-    def load(cls, path: str, native: Optional[bool] = None) -> "Ledger":
+    def load(cls, path: str, native: Optional[bool] = None, verify: bool = True) -> "Ledger":
+        """Load a JSONL chain. Rows are untrusted input: the chain is re-verified (heights,
+        prev-hash links, block hashes) before it is returned; ``verify=False`` only for forensics."""
         with open(path) as fh:
             rows = [json.loads(l) for l in fh if l.strip()]
         led = cls(native=native, truncate=False)
@@ -140,7 +142,30 @@ class Ledger:
         for r in rows:
             led._c.push_raw(r)
         led.path, led._flushed = path, len(rows)
+        if verify:
+            bad = led.verify()
+            if bad != -1:
+                raise ValueError(f"ledger {path} fails verification at height {bad}")
         return led
+
+    def truncated(self, height: int) -> "Ledger":
+        """A copy holding blocks [0, height) (resume: drop blocks appended after a checkpoint)."""
+        led = Ledger(native=self.native, truncate=False)
+        led._c.clear()
+        for i in range(min(height, len(self))):
+            led._c.push_raw(self.block(i))
+        return led
+
+    def rewrite(self):
+        """Rewrite the JSONL file from the in-memory chain."""
+        if not self.path:
+            return
+        tmp = self.path + ".tmp"
+        with open(tmp, "w") as fh:
+            for i in range(len(self)):
+                fh.write(json.dumps(self.block(i), sort_keys=True) + "\n")
+        os.replace(tmp, self.path)
+        self._flushed = len(self)
 
     def consensus_check(self) -> bool:
         """All ranks hold the same tip (ranks append identical blocks in identical order)."""

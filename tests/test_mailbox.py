@@ -37,7 +37,9 @@ def _transport_worker(rank, world):
         out = {peer: torch.zeros(1000)}
         got = tr.fetch({peer: 0}, out)
         again = tr.fetch({peer: 1}, out)  # nothing newer than version 1
-        # a half-written version: begin = 3 without end -> the reader keeps version 1
+        D.barrier()
+        # a half-written version 3 (begin without end) lands in slot 1, over version 1: the
+        # reader finds no complete snapshot and keeps what it holds
         tr.backend.hdr_store(tr.outbox[rank][0][1].hdr, 1, [3], 0)
         D.barrier()
         torn_view = tr.fetch({peer: 1}, out)
