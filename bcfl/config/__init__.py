@@ -49,6 +49,9 @@ class FLConfig:
     adam_eps: float = 1e-6
     adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
     keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
+    drift_correction: str = "none"      # none | scaffold (control variates in update space,
+                                        # fused into AdamW; no extra communication — fl/drift.py)
+    drift_correction_scale: float = 1.0
     dropout: Optional[float] = None     # None -> model default
     dtype: str = "bf16"                 # compute dtype on GPU ("bf16" | "fp32")
     # --- federation ------------------------------------------------------------
@@ -227,11 +230,14 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # constant-prediction plateau at that rate; the measured protocol that learns (MI355X sweeps,
     # profiles/accuracy_curves_*.json): lr 2e-5 with 3 rounds of linear warm-up, AdamW moments kept
     # per client across rounds, and a synthetic task whose planted class tokens are 12 per 64.
+    # Label-sharded clients (one class each) additionally need client-drift correction
+    # (SCAFFOLD control variates, bcfl/fl/drift.py): without it the mixed model collapses to the
+    # majority rate after every local epoch.
     "baseline3_learnable": dict(mode="serverless", model="bert-base", dataset="imdb", num_labels=2,
                                 num_clients=8, num_rounds=20, partition="label_shards",
                                 train_samples=240, test_samples=60, async_gossip=True, lr=2e-5,
-                                lr_warmup_steps=24, keep_optimizer_state=True, synthetic_signal=12.0,
-                                global_test_samples=1000),
+                                lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
+                                global_test_samples=1000, drift_correction="scaffold"),
     "baseline4_biobert_serverless_noniid_trust": dict(mode="serverless", model="biobert",
                                                       dataset="imdb", num_labels=2, num_clients=8,
                                                       num_rounds=20, partition="label_shards",

@@ -335,7 +335,8 @@ void adamw(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> para
 
 void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
               std::vector<Tensor> grads, std::vector<int64_t> offs, double lr, double b1, double b2,
-              double eps, double wd, int64_t step, int64_t mode, double grad_scale) {
+              double eps, double wd, int64_t step, int64_t mode, double grad_scale,
+              optional<Tensor> corr, double corr_lr) {
   check_cuda(master, "master");
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
               v.scalar_type() == at::kFloat, "AdamW state must be fp32");
@@ -354,12 +355,17 @@ void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
     numels.push_back(g.numel());
   }
   const bool po = param_out.has_value() && param_out->defined();
+  const bool hc = corr.has_value() && corr->defined();
+  if (hc)
+    TORCH_CHECK(corr->is_cuda() && corr->scalar_type() == at::kFloat && corr->is_contiguous() &&
+                corr->numel() == master.numel(), "drift correction must be a flat fp32 buffer");
   check_rc(bcfl::launch_adamw_mt(master.data_ptr<float>(), m.data_ptr<float>(),
                                  v.data_ptr<float>(), po ? param_out->data_ptr() : nullptr,
                                  po ? dt_of(*param_out) : -1, ptrs.data(), offs.data(),
                                  numels.data(), (int)ptrs.size(), gdt, (float)lr, (float)b1,
                                  (float)b2, (float)eps, (float)wd, (int)step, (int)mode,
-                                 (float)grad_scale, stream()),
+                                 (float)grad_scale, hc ? corr->data_ptr<float>() : nullptr,
+                                 (float)corr_lr, stream()),
            "adamw_mt");
 }
 

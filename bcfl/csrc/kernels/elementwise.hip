@@ -331,7 +331,9 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
     float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
     bf16_t* __restrict__ pout_bf, float* __restrict__ pout_f, MTArgs a, int64_t chunk, float b1,
     float b2, float eps, float step_size, float decay_mul, float denom_scale, int hf,
-    float grad_scale) {
+    float grad_scale, const float* __restrict__ corr, float corr_lr) {
+  // corr (optional): drift-correction direction in update space (SCAFFOLD-style control variate
+  // difference c - c_i, bcfl/fl/drift.py); the step becomes p -= lr * (adam_update + corr)
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   int64_t hi = lo + chunk;
   if (hi > a.start[a.n]) hi = a.start[a.n];
@@ -354,6 +356,12 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
       for (int k = 0; k < 4; ++k)
         adam_elem(p[k], gv[k] * grad_scale, mm[k], vv[k], b1, b2, eps, step_size, decay_mul,
                   denom_scale, hf);
+      if (corr) {
+        float cv[4];
+        Vec4<float>::load(corr + f, cv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] -= corr_lr * cv[k];
+      }
       Vec4<float>::store(master + f, p);
       Vec4<float>::store(m + f, mm);
       Vec4<float>::store(v + f, vv);
@@ -364,6 +372,7 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
         float p = master[f + k], mm = m[f + k], vv = v[f + k];
         adam_elem(p, ld<TG>(g, k) * grad_scale, mm, vv, b1, b2, eps, step_size, decay_mul,
                   denom_scale, hf);
+        if (corr) p -= corr_lr * corr[f + k];
         master[f + k] = p;
         m[f + k] = mm;
         v[f + k] = vv;
@@ -550,7 +559,8 @@ int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* 
 int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int param_dt,
                     const void* const* grads, const int64_t* offs, const int64_t* numels,
                     int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
-                    int step, int mode, float grad_scale, hipStream_t s) {
+                    int step, int mode, float grad_scale, const float* corr, float corr_lr,
+                    hipStream_t s) {
   const double bc1 = 1.0 - __builtin_pow((double)b1, step);
   const double bc2 = 1.0 - __builtin_pow((double)b2, step);
   const int hf = mode == 0;
@@ -578,11 +588,11 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
     if (grad_dt == DT_BF16)
       hipLaunchKernelGGL(adamw_mt_kernel<bf16_t>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
                          pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
-                         grad_scale);
+                         grad_scale, corr, corr_lr);
     else
       hipLaunchKernelGGL(adamw_mt_kernel<float>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
                          pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
-                         grad_scale);
+                         grad_scale, corr, corr_lr);
   }
   return 0;
 }

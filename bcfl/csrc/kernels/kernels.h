@@ -63,7 +63,8 @@ int launch_adamw(float* master, const void* grad, int grad_dt, float* m, float* 
 int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int param_dt,
                     const void* const* grads, const int64_t* offs, const int64_t* numels,
                     int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
-                    int step, int mode, float grad_scale, hipStream_t s);
+                    int step, int mode, float grad_scale, const float* corr, float corr_lr,
+                    hipStream_t s);
 int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
                         float* out, hipStream_t s);
 

@@ -44,6 +44,7 @@ from ..parallel.topology import clients_of_rank, mixing_matrix, neighbours
 from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
 from ..utils.obs import MetricsWriter, PhaseTimer, Telemetry
+from .drift import DriftCorrection
 from .trainer import EvalResult, LocalTrainer
 
 DATA_SEED = 1234
@@ -140,6 +141,8 @@ class Federation:
             for c in self.local_clients:
                 self.client_master[c] = self.flat.master.detach().clone()
         self.lanes = self._build_lanes(vocab, mdtype)
+        self.drift = DriftCorrection(cfg.drift_correction, cfg.drift_correction_scale,
+                                     self.local_clients, self.flat.numel, self.device)
         ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else len(self.lanes) <= 1
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
         self.global_master: Optional[torch.Tensor] = None
@@ -273,6 +276,7 @@ class Federation:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
+                self.drift.attach(lane.opt, c)
                 prev = lane.flat.master.detach().clone() if need_prev else None
                 loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
             st = {"batches": 0, "tokens": 0, "examples": 0}
@@ -298,6 +302,8 @@ class Federation:
             if c in cfg.inject_slow:
                 time.sleep(cfg.inject_slow[c] / 1000.0)
             with self._on(lane):
+                self.drift.after_train(c, lane.flat.master, self.lr_sum(r, st["batches"]))
+                self.drift.detach(lane.opt)
                 if prev is not None:
                     self._inject_byzantine(c, prev, lane.flat)
                     if self.filter is not None:
@@ -374,6 +380,10 @@ class Federation:
             return lo + (c.lr - lo) * 0.5 * (1.0 + math.cos(math.pi * t))
         raise KeyError(f"unknown lr_schedule {c.lr_schedule!r}")
 
+    def lr_sum(self, r: int, steps: int) -> float:
+        """Sum of the learning rates of round r's first ``steps`` local steps (drift correction)."""
+        return float(sum(self.lr_at(r, i) for i in range(steps)))
+
     def client_examples(self, c: int, r: int) -> int:
         return int(len(self.partitions(r)[c].train))
 
@@ -431,6 +441,7 @@ class Federation:
             self.opt.load_state_dict(self.client_opt[c])
         else:
             self.opt.reset()
+        self.drift.attach(self.opt, c)
         ops.rng.global_rng().load_state(self.client_rng[c])
 
     def _deactivate(self, c: int):
@@ -535,6 +546,8 @@ class Federation:
             if self.verbose and cfg.reference_prints:
                 print("Training Started...", flush=True)
             st = self._train_client(c, r)
+            self.drift.after_train(c, self.flat.master, self.lr_sum(r, st["batches"]))
+            self.drift.detach(self.opt)
             self._inject_byzantine(c, G)
             if self.verbose and cfg.reference_prints:
                 print("Training Finished.", flush=True)
@@ -566,6 +579,8 @@ class Federation:
             D.all_reduce_(self.acc)
         G.copy_(self.acc)
         self.flat.load_master(G)
+        for c in self.local_clients:
+            self.drift.after_mix(c, G)
         # Flower evaluate_round: every client evaluates the new global model on its test split
         client_metrics = []
         if cfg.eval_local:
@@ -649,6 +664,8 @@ class Federation:
             self._activate(c)
             prev = self.flat.master.detach().clone() if need_prev else None
             st = self._train_client(c, r)
+            self.drift.after_train(c, self.flat.master, self.lr_sum(r, st["batches"]))
+            self.drift.detach(self.opt)
             if prev is not None:
                 self._inject_byzantine(c, prev)
                 if self.filter is not None:
@@ -674,6 +691,8 @@ class Federation:
                                             steps={c: losses[c]["batches"] for c in losses})
         recs += self._gossip_records(r, recs)
         self.prev_verdicts = v
+        for c in self.local_clients:
+            self.drift.after_mix(c, self.client_master[c] if self.multi else self.flat.master)
         if self.multi:  # evaluate this rank's first client's mixed model
             self.flat.load_master(self.client_master[self.local_clients[0]])
         ge = self._eval_global(r) if cfg.eval_global else None
@@ -811,6 +830,7 @@ class Federation:
               "client_opt": {int(c): {"m": cpu(o["m"]), "v": cpu(o["v"]), "step": int(o["step"])}
                              for c, o in self.client_opt.items()},
               "prev_rejected": sorted(self.prev_verdicts.rejected),
+              "drift": self.drift.state_dict(),
               "tokens_trained": int(self.tokens_trained)}
         if self.global_master is not None:
             st["global_master"] = cpu(self.global_master)
@@ -935,6 +955,7 @@ class Federation:
         if self.global_master is not None and "global_master" in st:
             self.global_master.copy_(st["global_master"])
         self.prev_verdicts = Verdicts(rejected=set(int(x) for x in st.get("prev_rejected", [])))
+        self.drift.load_state_dict(st.get("drift"))
         self.tokens_trained = int(st.get("tokens_trained", 0))
         if self.gossip is not None and "gossip" in st:
             self.gossip.load_state_dict(st["gossip"])

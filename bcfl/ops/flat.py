@@ -34,21 +34,30 @@ def adamw_(master, grad, m, v, step: int, lr: float, beta1: float, beta2: float,
 def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], m, v, step: int,
                  lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
                  mode: str = "hf", param_out: Optional[torch.Tensor] = None,
-                 grad_scale: float = 1.0):
+                 grad_scale: float = 1.0, corr: Optional[torch.Tensor] = None,
+                 corr_lr: float = 0.0):
     """AdamW where each gradient is its own tensor (as autograd produced it) and master / m / v /
-    param live in flat buffers at ``offsets``: one multi-tensor launch per <=48 tensors."""
+    param live in flat buffers at ``offsets``: one multi-tensor launch per <=40 tensors.
+
+    ``corr`` (flat fp32, optional): drift correction in update space, applied in the same pass as
+    ``p -= corr_lr * corr`` on every element that received a gradient (bcfl.fl.drift)."""
     if not grads:
         return
     if use_native(master, "adamw"):
         native().adamw_mt(master, m, v, param_out, list(grads), [int(o) for o in offsets],
                           float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-                          int(step), 0 if mode == "hf" else 1, float(grad_scale))
+                          int(step), 0 if mode == "hf" else 1, float(grad_scale), corr,
+                          float(corr_lr))
         return
     for g, o in zip(grads, offsets):
         n = g.numel()
         po = None if param_out is None or param_out.data_ptr() == master.data_ptr() else param_out[o:o + n]
         ref.adamw_(master[o:o + n], g.reshape(-1), m[o:o + n], v[o:o + n], step, lr, beta1, beta2,
-                   eps, weight_decay, mode, po, grad_scale)
+                   eps, weight_decay, mode, None if corr is not None else po, grad_scale)
+        if corr is not None:
+            master[o:o + n].sub_(corr[o:o + n], alpha=corr_lr)
+            if po is not None:
+                po.copy_(master[o:o + n])
 
 
 def gossip_mix_(master: torch.Tensor, neighbours: Sequence[torch.Tensor], self_w: float,

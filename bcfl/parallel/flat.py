@@ -122,6 +122,10 @@ class FlatAdamW:
         self.m = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.v = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.step_count = 0
+        # drift correction (bcfl.fl.drift): flat fp32 update-space direction added to every step
+        # as p -= lr * corr_scale * corr, fused into the AdamW kernel; None = off
+        self.corr: Optional[torch.Tensor] = None
+        self.corr_scale = 1.0
 
     def reset(self):
         self.m.zero_()
@@ -136,7 +140,8 @@ class FlatAdamW:
         ops.adamw_multi_(f.master, grads, offs, self.m, self.v, self.step_count, self.lr,
                          self.betas[0], self.betas[1], self.eps, self.wd, self.mode,
                          param_out=None if f.master is f.param else f.param,
-                         grad_scale=grad_scale)
+                         grad_scale=grad_scale, corr=self.corr,
+                         corr_lr=self.lr * self.corr_scale)
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}

@@ -29,12 +29,12 @@ BASELINE_S_PER_ROUND = (27.8 + (40.0 - 27.8) * (8 - 5) / (10 - 5)) / 20.0 * 60.0
 BASELINE_FINAL_ACC = 0.54
 ACCURACY_NOTE = (
     "synthetic IMDB-shaped data + random-init BERT-base; final_accuracy is scored on a "
-    "class-balanced global draw (final_majority_rate = what a constant predictor scores). With "
-    "label-sharded Non-IID clients (every client sees ONE class) a random-init 12-layer BERT does "
-    "not learn within the bench's rounds - the reference's own serverless Non-IID result is 54% "
-    "on a 2-class task. Learning curves under the documented random-init protocol (IID and "
-    "Non-IID, server and serverless) are in profiles/accuracy_curves_*.json "
-    "(benchmarks/accuracy_curves.py)")
+    "class-balanced 1000-row global draw (final_majority_rate = what a constant predictor "
+    "scores). Label-sharded Non-IID clients (each client sees ONE class) collapse to the majority "
+    "rate under plain gossip averaging; the bench's protocol adds SCAFFOLD-style client-drift "
+    "correction (update-space control variates fused into AdamW, no extra communication, "
+    "bcfl/fl/drift.py) with the reference's fresh AdamW per round. 25-round curves on MI355X with "
+    "and without it: profiles/accuracy_curves_scaffold_mi355x.json (benchmarks/accuracy_curves.py)")
 
 
 def parse():
@@ -152,6 +152,7 @@ def main():
                                   "lr_warmup_steps": cfg.lr_warmup_steps,
                                   "keep_optimizer_state": cfg.keep_optimizer_state,
                                   "synthetic_signal": cfg.synthetic_signal,
+                                  "drift_correction": cfg.drift_correction,
                                   "rounds_trained": a.warmup + a.steps},
             "tokens_per_s": tokens / dt,
             "samples_per_s": a.clients * cfg.train_samples * a.steps / dt,

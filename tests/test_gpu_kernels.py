@@ -212,8 +212,8 @@ def test_fused_adamw(mode):
     _close(p_out, rm, 1e-2)
 
 
-@pytest.mark.parametrize("mode", ["hf", "torch"])
-def test_multi_tensor_adamw(mode):
+@pytest.mark.parametrize("mode,with_corr", [("hf", False), ("torch", False), ("hf", True)])
+def test_multi_tensor_adamw(mode, with_corr):
     torch.manual_seed(0)
     sizes = [768, 2, 3072 * 768, 5, 30522 * 768, 64] + [777] * 45  # > one 40-tensor group
     offs, o = [], 0
@@ -224,13 +224,18 @@ def test_multi_tensor_adamw(mode):
     m, v = torch.zeros(o, device=DEV), torch.zeros(o, device=DEV)
     p_out = torch.zeros(o, device=DEV, dtype=torch.bfloat16)
     rm, rmm, rvv = master.clone(), m.clone(), v.clone()
+    # drift correction (fl/drift.py): p -= corr_lr * corr fused into the same pass
+    corr = torch.randn(o, device=DEV) if with_corr else None
     for t in range(1, 3):
         grads = [torch.randn(n, device=DEV).bfloat16() for n in sizes]
-        ops.adamw_multi_(master, grads, offs, m, v, t, 1e-3, 0.9, 0.999, 1e-6, 0.01, mode, p_out)
+        ops.adamw_multi_(master, grads, offs, m, v, t, 1e-3, 0.9, 0.999, 1e-6, 0.01, mode, p_out,
+                         corr=corr, corr_lr=5e-4)
         for g, of in zip(grads, offs):
             n = g.numel()
             ref.adamw_(rm[of:of + n], g.float(), rmm[of:of + n], rvv[of:of + n], t, 1e-3, 0.9,
                        0.999, 1e-6, 0.01, mode)
+            if corr is not None:
+                rm[of:of + n] -= 5e-4 * corr[of:of + n]
     _close(master, rm, 1e-5, 1e-5)
     _close(m, rmm, 1e-6, 1e-5)
     mask = torch.zeros(o, dtype=torch.bool, device=DEV)

@@ -60,8 +60,9 @@ def test_mailbox_transport_post_fetch(tmp_path):
         assert int(r["again"]) == 0 and int(r["half"]) == 0
 
 
-def _fed_worker(rank, world, out, kw, stop_after=None):
+def _fed_worker(rank, world, out, kw, stop_after=None, test_barrier=False):
     from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
     fed = Federation(_cfg(out, **kw), verbose=False)
     times = []
     for r in range(fed.cfg.num_rounds):
@@ -70,6 +71,10 @@ def _fed_worker(rank, world, out, kw, stop_after=None):
         t0 = time.perf_counter()
         fed.run_round(r)
         times.append(time.perf_counter() - t0)
+        if test_barrier:
+            # test-only: make round r's posts visible before round r+1 fetches, so the assertion
+            # on accepted updates does not depend on process scheduling (the protocol never waits)
+            D.barrier()
     fed.finish(audit=stop_after is None)
     blocks = fed.ledger.blocks() if fed.ledger is not None else []
     return {"master": fed.flat.master.clone(), "times": torch.tensor(times),
@@ -83,7 +88,7 @@ def _fed_worker(rank, world, out, kw, stop_after=None):
 
 
 def test_mailbox_federation_async_runs(tmp_path):
-    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), {})
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), {}, None, True)
     for r in res:
         assert torch.isfinite(r["master"]).all()
         assert int(r["accepts"]) >= 1 and int(r["rejects"]) == 0
