@@ -31,7 +31,8 @@ class FLConfig:
     batch_size: int = 32
     max_seq_len: int = 512
     # --- data partitioning ---------------------------------------------------
-    partition: str = "label_shards"     # iid_random | ref_contiguous | label_shards | dirichlet | shared_random
+    partition: str = "label_shards"     # iid_random | ref_contiguous | label_shards | dirichlet |
+                                        # shared_random | ref_shared_prefix
     train_samples: int = 240            # per client
     test_samples: int = 60              # per client (local eval)
     global_test_samples: int = 100      # global eval draw (reference load_data(): 100)
@@ -56,19 +57,20 @@ class FLConfig:
     dtype: str = "bf16"                 # compute dtype on GPU ("bf16" | "fp32")
     # --- federation ------------------------------------------------------------
     topology: str = "full"              # full | ring | pagerank (serverless neighbour graph)
-    mixing: str = "average"             # average (reference mean) | metropolis | choco
-    choco_gamma: float = 0.5
+    mixing: str = "average"             # average (reference mean) | metropolis
     async_gossip: bool = True           # exchange on the side stream, mix stale-by-one replicas
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
                                         # (matched send/recv); auto = mailbox when async, else rccl
     verify_updates: bool = True         # receivers re-hash every received payload vs its root
     wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
-    server_wire_dtype: str = "fp32"
+    server_wire_dtype: str = "fp32"     # server FedAvg reduction on the wire: fp32 all-reduce |
+                                        # bf16 (delta-coded all-to-all + all-gather, fp32 accumulate)
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
     client_lanes: int = 0               # concurrent client lanes per rank (own replica + HIP stream);
-                                        # 0 = auto (min(8, hosted clients) on GPU, 1 on CPU)
+                                        # 0 = auto: min(8, hosted) on GPU (min(2, hosted) for
+                                        # models > 1e9 parameters: activation memory), 1 on CPU
     # --- trust layer -------------------------------------------------------------
     anomaly_filter: str = "none"        # none | pagerank | modz | both
     anomaly_k: float = 2.0              # reject below mean - k*std of PageRank
@@ -98,7 +100,9 @@ class FLConfig:
     sweep_clients: List[int] = field(default_factory=list)  # run once per client count (C19)
     profile: bool = False
     progress: bool = False              # per-client / per-round progress lines (long rounds)
-    deterministic: bool = False
+    deterministic: bool = False         # bit-reproducible runs: async gossip uses the lock-step
+                                        # RCCL engine (staleness exactly 1 round) instead of the
+                                        # timing-dependent mailbox; torch deterministic algorithms
     seed: int = 42
     device: str = "auto"                # auto | cuda | cpu
     backend: str = "auto"               # auto | nccl | gloo
@@ -109,6 +113,23 @@ class FLConfig:
     vocab_size: Optional[int] = None
     lora_rank: int = 16
     lora_alpha: float = 32.0
+
+    def __post_init__(self):
+        choices = {"mode": ("server", "serverless"), "mixing": ("average", "metropolis"),
+                   "topology": ("full", "ring", "pagerank"),
+                   "gossip_transport": ("auto", "mailbox", "rccl"),
+                   "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
+                   "drift_correction": ("none", "scaffold"), "adam_mode": ("hf", "torch"),
+                   "lr_schedule": ("constant", "linear", "cosine"),
+                   "anomaly_filter": ("none", "pagerank", "modz", "both"),
+                   "fedavg_weighting": ("examples", "batches", "uniform")}
+        for k, allowed in choices.items():
+            if getattr(self, k) not in allowed:
+                raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")
+        if self.deterministic and self.async_gossip and self.gossip_transport == "mailbox":
+            raise ValueError("deterministic=True needs a fixed gossip schedule: the one-sided "
+                             "mailbox mixes whatever snapshot is newest (timing-dependent); use "
+                             "gossip_transport=auto/rccl (async = staleness exactly one round)")
 
     def to_dict(self) -> Dict[str, Any]:
         d = dataclasses.asdict(self)
@@ -250,6 +271,24 @@ PRESETS: Dict[str, Dict[str, Any]] = {
                                                 train_samples=240, test_samples=60, batch_size=8,
                                                 max_seq_len=512, lr=2e-4),
 }
+
+# Reference-faithful ("_compat") variants of the three scripts whose data handling differs from
+# what their names say. The un-suffixed presets above keep the INTENDED semantics (a real
+# Non-IID split); these reproduce what the scripts actually run.
+PRESETS.update({
+    # src/Servercase/server_NonIID_IMDB.py:68,83-84,224-227: load_data_count(0) once on the
+    # shuffled split -> all 20 clients share train rows [0,240) and test rows [240,300) (IID)
+    "server_NonIID_IMDB_compat": {**PRESETS["server_NonIID_IMDB"], "partition": "ref_shared_prefix"},
+    # src/Servercase/server_noniid_medical_transcriptions.py:86-91,219-221: the unused Non-IID
+    # loader aside, the script runs the IID load_data(): ONE random 1000/1000 draw, shared
+    "server_noniid_medical_transcriptions_compat": {
+        **PRESETS["server_noniid_medical_transcriptions"], "partition": "shared_random",
+        "train_samples": 1000, "test_samples": 1000},
+    # src/Serverlesscase/serverless_NonIID_IMDB.py:48,59-60: contiguous shards of the UNSHUFFLED
+    # (label-sorted) split -> every client's 240 rows are label 0
+    "serverless_NonIID_IMDB_compat": {**PRESETS["serverless_NonIID_IMDB"],
+                                      "partition": "ref_contiguous"},
+})
 
 # README.md:2-5 canonical entry-point names
 PRESETS["server_IID"] = PRESETS["server_IID_IMDB"]

@@ -11,6 +11,11 @@
                         ``Serverless_NonIID_Medical_transcriptions.py:55-56``: train
                         ``[500k, 500k+400)``, test ``[0, 400)``). On label-sorted IMDB every
                         shard is single-class label 0 — reproduced on purpose.
+* ``ref_shared_prefix`` — reference ``load_data_count(0)`` of ``server_NonIID_IMDB.py:65-101``:
+                        the split is SHUFFLED once (``.shuffle(seed=42)``, :68) and EVERY client gets
+                        the same rows — train ``[0, 240)``, test ``[240, 300)`` (:83-84, called once
+                        at :224, ``client_fn`` returns the same loaders for every cid) — so the
+                        script named "NonIID" is in fact IID with shared data. Reproduced on purpose.
 * ``label_shards``    — pathological Non-IID spread over the whole label-sorted split: shard k is
                         the head of the k-th of ``num_clients`` equal contiguous blocks, so clients
                         see different single classes (what a Non-IID benchmark intends).
@@ -86,6 +91,13 @@ def partition_clients(kind: str, spec: DatasetSpec, train_labels: np.ndarray,
             else:
                 te = np.arange(0, min(ln, n_te))
             splits.append(ClientSplit(tr.astype(np.int64), te.astype(np.int64)))
+    elif kind == "ref_shared_prefix":
+        r = _rng(seed, 4242)
+        stride, ln = spec.ref_train_stride, spec.ref_train_len
+        ptr, pte = r.permutation(n_tr), r.permutation(n_te)
+        tr = np.sort(ptr[:min(ln, n_tr)]).astype(np.int64)
+        te = np.sort(pte[ln:min(stride, n_te)]).astype(np.int64)
+        splits = [ClientSplit(tr, te) for _ in range(num_clients)]
     elif kind == "label_shards":
         for k in range(num_clients):
             blk_tr = n_tr // num_clients

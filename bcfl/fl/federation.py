@@ -102,6 +102,12 @@ class Federation:
         self.is_cuda = self.device.type == "cuda"
         self.verbose = verbose and self.rt.is_main
         self.dtype = torch.bfloat16 if (self.is_cuda and cfg.dtype == "bf16") else torch.float32
+        if self.is_cuda and cfg.dtype == "fp32" and not cfg.model.startswith("llama"):
+            raise ValueError("dtype='fp32' on the GPU: the bcfl MFMA kernels (attention, wgrad, "
+                             "fused LayerNorm) compute in bf16 with fp32 accumulation and fp32 "
+                             "master weights; use dtype='bf16' (fp32 runs on device='cpu')")
+        if cfg.deterministic:
+            torch.use_deterministic_algorithms(True, warn_only=True)
         self.telemetry = Telemetry()
         # ---------------- data --------------------------------------------------------------
         self.spec = get_dataset(cfg.dataset)
@@ -154,7 +160,8 @@ class Federation:
             raise ValueError(f"unknown gossip_transport {cfg.gossip_transport!r}")
         self.transport = cfg.gossip_transport
         if self.transport == "auto":
-            self.transport = "mailbox" if cfg.async_gossip else "rccl"
+            # deterministic: the lock-step engine mixes exactly the previous round's states
+            self.transport = "mailbox" if (cfg.async_gossip and not cfg.deterministic) else "rccl"
         # A mailbox federation never waits on a peer: the per-round path is collective-free
         # (metrics, evaluation and ledger are rank-local) so a slow or exited rank cannot stall
         # the others. The update anomaly filter needs a global view and keeps its collectives.
@@ -576,7 +583,16 @@ class Federation:
             for x in recs:
                 x["verdict"] = v.verdict(x["client"])
         with self.timer.phase("comm"):
-            D.all_reduce_(self.acc)
+            if cfg.server_wire_dtype == "bf16" and self.rt.distributed:
+                # delta coding: each rank reduces sum_{k local} w_k (x_k - G), bf16 on the wire
+                wloc = float(sum(w[c] for c in self.local_clients)) if self.filter is not None \
+                    else float(sum(w_all[c] for c in self.local_clients))
+                ops.axpby_(self.acc, G, -wloc, 1.0)
+                wire_bytes = D.all_reduce_bf16_(self.acc)
+                ops.axpby_(self.acc, G, 1.0, 1.0)
+            else:
+                D.all_reduce_(self.acc)
+                wire_bytes = self.acc.numel() * 4 * 2 * max(self.rt.world - 1, 0) // max(self.rt.world, 1)
         G.copy_(self.acc)
         self.flat.load_master(G)
         for c in self.local_clients:
@@ -601,7 +617,7 @@ class Federation:
                                      "rejected": sorted(v.rejected)})
         return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
-                "client_metrics": client_metrics, "bytes_sent": float(self.flat.nbytes("master"))}
+                "client_metrics": client_metrics, "bytes_sent": float(wire_bytes)}
 
     @property
     def _gossip_roots(self) -> bool:

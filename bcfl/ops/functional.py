@@ -54,7 +54,9 @@ def wgrad(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 # attention / LayerNorm backward kernels; the weight gradients hang off it and are only needed
 # by the optimizer. With overlap on, each dW (+db) is launched on a side HIP stream paired with
 # the stream autograd runs on, so the K9 kernels fill the CUs the (often sub-wave) dgrad GEMMs
-# leave idle; :func:`join_wgrad` makes the optimizer's stream wait for them.
+# leave idle; :func:`join_wgrad` makes the optimizer's stream wait for them. Contract: while
+# overlap is on, every backward() must be followed by join_wgrad() before the gradients are read
+# (LocalTrainer.step does this); parameters that already hold a .grad take the inline path.
 # ----------------------------------------------------------------------------------------
 _WG = {"enabled": False, "side": {}}
 
@@ -115,6 +117,7 @@ class _Linear(torch.autograd.Function):
         # a parameter used several times per step gets its gradients summed by autograd on
         # autograd's stream, which a side-stream dW would race with
         ctx.shared = getattr(w, "_bcfl_shared", False) or getattr(b, "_bcfl_shared", False)
+        ctx.bias = b
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -127,8 +130,12 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = g2.mm(w).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if (ctx.needs_input_grad[1] and _WG["enabled"] and not ctx.shared and use_native(g2)
-                and wgrad_supported(g2, x2)):
+        # The side-stream dW is only safe when AccumulateGrad STEALS it (no .grad yet): if a
+        # gradient is already there, autograd adds into it on its own stream, reading dW before
+        # the side-stream kernel finished -> compute it inline instead.
+        steal = w.grad is None and (ctx.bias is None or ctx.bias.grad is None)
+        if (ctx.needs_input_grad[1] and _WG["enabled"] and not ctx.shared and steal
+                and use_native(g2) and wgrad_supported(g2, x2)):
             dw, db = _wgrad_async(g2, x2, want_b)
         elif ctx.needs_input_grad[1]:
             if want_b and use_native(g2) and wgrad_supported(g2, x2):

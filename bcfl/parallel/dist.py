@@ -106,6 +106,31 @@ def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
     return dist.all_reduce(t, op=op, async_op=async_op)
 
 
+def all_reduce_bf16_(x: torch.Tensor) -> int:
+    """Sum a flat fp32 tensor over ranks with bf16 on the wire and fp32 accumulation.
+
+    Reduce-scatter as an all-to-all of bf16 chunks (every rank receives all ranks' copy of ITS
+    1/world chunk and sums them in fp32), then an all-gather of the bf16-rounded chunk sums:
+    2 (world-1)/world x 2 B per element on the wire — half of a ring fp32 all-reduce — and only
+    ONE bf16 rounding per element (a bf16 ring all-reduce would round at every hop). Meant for
+    DELTAS (FedAvg: sum_k w_k (x_k - G)), whose bf16 rounding is relative to the update, not to
+    the weights. Returns the bytes this rank put on the wire."""
+    rt = runtime()
+    if not rt.distributed:
+        return 0
+    W, n = rt.world, x.numel()
+    per = -(-n // W)
+    send = torch.zeros(W * per, dtype=torch.bfloat16, device=x.device)
+    send[:n].copy_(x.reshape(-1))
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    part = recv.view(W, per).float().sum(0).to(torch.bfloat16)
+    out = torch.empty_like(send)
+    dist.all_gather_into_tensor(out, part)
+    x.reshape(-1).copy_(out[:n])
+    return 2 * (W - 1) * per * 2
+
+
 def broadcast_(t: torch.Tensor, src: int = 0):
     if runtime().distributed:
         dist.broadcast(t, src=src)

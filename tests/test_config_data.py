@@ -98,3 +98,49 @@ def test_client_loader_epochs():
     b1 = ld.device_batches("cpu", epoch=1)
     assert [b.batch_size for b in b0] == [32, 32, 6]
     assert not torch.equal(b0[0].labels, b1[0].labels) or not torch.equal(b0[0].input_ids, b1[0].input_ids)
+
+
+def test_config_rejects_unknown_choices():
+    import pytest
+    from bcfl.config import FLConfig
+    for kw in ({"mixing": "choco"}, {"server_wire_dtype": "fp16"}, {"drift_correction": "x"},
+               {"mode": "p2p"},
+               {"deterministic": True, "async_gossip": True, "gossip_transport": "mailbox"}):
+        with pytest.raises(ValueError):
+            FLConfig(**kw)
+    FLConfig(deterministic=True, async_gossip=True)  # auto transport -> lock-step engine
+
+
+def test_compat_presets_reproduce_reference_partitions():
+    """Per-script partition semantics: the _compat presets run what the
+    reference scripts actually do; the plain presets keep a real Non-IID split."""
+    import numpy as np
+    from bcfl.data.partition import partition_clients
+    from bcfl.data.registry import get_dataset, load_split
+
+    def parts(name, n=None):
+        cfg = get_preset(name)
+        spec = get_dataset(cfg.dataset)
+        tr = load_split(cfg.dataset, "train", 30522, 128, 1234, 101, 102)
+        te = load_split(cfg.dataset, "test", 30522, 128, 1234, 101, 102)
+        return cfg, tr, partition_clients(cfg.partition, spec, tr.labels, te.labels,
+                                          n or cfg.num_clients, cfg.train_samples,
+                                          cfg.test_samples, cfg.seed)
+
+    # E2 compat: every client holds the same 240 / 60 rows of the shuffled split, both classes
+    cfg, tr, ps = parts("server_NonIID_IMDB_compat")
+    assert len(ps) == 20 and all(np.array_equal(p.train, ps[0].train) for p in ps)
+    assert len(ps[0].train) == 240 and len(ps[0].test) == 60
+    assert len(np.unique(tr.labels[ps[0].train])) == 2
+    # E4 compat: one shared IID 1000/1000 draw
+    cfg, tr, ps = parts("server_noniid_medical_transcriptions_compat")
+    assert all(np.array_equal(p.train, ps[0].train) for p in ps) and len(ps[0].train) == 1000
+    assert len(np.unique(tr.labels[ps[0].train])) > 20
+    # E6 compat: contiguous unshuffled shards [300k, 300k+240) -> all label 0 on label-sorted IMDB
+    cfg, tr, ps = parts("serverless_NonIID_IMDB_compat")
+    assert [int(p.train[0]) for p in ps[:3]] == [0, 300, 600]
+    assert all((tr.labels[p.train] == 0).all() for p in ps)
+    # the plain Non-IID presets: clients see different single classes
+    cfg, tr, ps = parts("serverless_NonIID_IMDB")
+    assert {int(tr.labels[p.train][0]) for p in ps} == {0, 1}
+    assert all(len(np.unique(tr.labels[p.train])) == 1 for p in ps)

@@ -193,3 +193,42 @@ def test_info_passing_benchmark_gloo(tmp_path):
     for s in res["sources"]:
         assert s["measured_sync_s"] > 0 and s["measured_async_s"] > 0
         assert s["predicted_async_s"] <= s["predicted_sync_s"]
+
+
+def test_server_bf16_wire_close_to_fp32(tmp_path):
+    """server_wire_dtype=bf16: delta-coded all-to-all + all-gather (fp32 accumulate, half the
+    wire bytes) lands within bf16 rounding of the UPDATE of the fp32 all-reduce result."""
+    res = run_world(_fed_worker, 2, str(tmp_path / "d"), "server", str(tmp_path / "d"),
+                    {"server_wire_dtype": "bf16"})
+    assert torch.equal(res[0]["master"], res[1]["master"])  # every rank ends on the same model
+    ref = run_world(_fed_worker, 2, str(tmp_path / "r"), "server", str(tmp_path / "r"), {})
+    from bcfl.models import build_model
+    init = torch.cat([p.detach().reshape(-1) for p in build_model("tiny-bert", 2, seed=42).parameters()])
+    upd = (ref[0]["master"] - res[0]["master"]).abs().max()
+    step = (ref[0]["master"][: init.numel()] - init).abs().max()
+    assert 0 < upd <= 0.02 * step
+
+
+def test_all_reduce_bf16_matches_sum(tmp_path):
+    res = run_world(_bf16_ar_worker, 3, str(tmp_path))
+    want = sum(torch.linspace(-1, 1, 1001) * (r + 1) for r in range(3))
+    for r in res:
+        assert torch.allclose(r, want, rtol=1e-2, atol=1e-2)
+        assert torch.equal(r, res[0])
+
+
+def _bf16_ar_worker(rank, world):
+    from bcfl.parallel import dist as D
+    D.init_runtime("cpu", "gloo")
+    x = torch.linspace(-1, 1, 1001) * (rank + 1)
+    nbytes = D.all_reduce_bf16_(x)
+    assert nbytes == 2 * (world - 1) * 334 * 2
+    return x
+
+
+def test_deterministic_async_is_reproducible(tmp_path):
+    kw = {"async_gossip": True, "deterministic": True, "num_rounds": 3}
+    a = run_world(_fed_worker, 2, str(tmp_path / "a"), "serverless", str(tmp_path / "a"), kw)
+    b = run_world(_fed_worker, 2, str(tmp_path / "b"), "serverless", str(tmp_path / "b"), kw)
+    for x, y in zip(a, b):
+        assert torch.equal(x["master"], y["master"])

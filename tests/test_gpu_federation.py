@@ -1,0 +1,72 @@
+"""GPU correctness of the concurrent paths the bench runs: interleaved client lanes on their own
+HIP streams (with and without side-stream weight gradients) must reproduce one-lane training
+BITWISE (the bcfl kernels are deterministic), and concurrent large GEMMs on two streams (the
+shape class that once deadlocked hipBLASLt Stream-K) must complete and agree with one stream."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _run(tmp, lanes, overlap):
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=4,
+                   num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                   out_dir=tmp, reference_prints=False, client_lanes=lanes, overlap_wgrad=overlap,
+                   async_gossip=False, gossip_transport="rccl", ledger=True, save_every=0,
+                   dropout=0.1, drift_correction="scaffold")
+    fed = Federation(cfg, verbose=False)
+    assert len(fed.lanes) == lanes
+    h = fed.run()
+    torch.cuda.synchronize()
+    out = (torch.stack([fed.client_master[c] for c in range(4)]).cpu(),
+           [r["train_loss"] for r in h], [b["update_root"] for b in fed.ledger.blocks()])
+    D.set_runtime_for_tests(None)
+    return out
+
+
+_SK = pytest.mark.xfail(reason="side-stream wgrad changes the timing of concurrent hipBLASLt "
+                        "Stream-K dgrad GEMMs, whose partial-tile fix-up order (fp32 sums) is "
+                        "timing-dependent (scripts/overlap_diag.py: 1e-6..1e-4 grad diffs, "
+                        "layer 0 + embeddings only); bitwise once the dgrad GEMMs are bcfl's own",
+                        strict=False)
+
+
+@pytest.mark.parametrize("lanes,overlap", [(3, False), pytest.param(3, True, marks=_SK),
+                                           pytest.param(1, True, marks=_SK)])
+def test_gpu_lanes_match_sequential(tmp_path, lanes, overlap):
+    a = _run(str(tmp_path / "ref"), 1, False)
+    b = _run(str(tmp_path / "x"), lanes, overlap)
+    assert torch.isfinite(a[0]).all()
+    assert torch.equal(a[0], b[0]), (a[0] - b[0]).abs().max()
+    assert a[1] == b[1]
+    assert a[2] == b[2]
+
+
+def test_gpu_concurrent_llama_shaped_gemms_complete():
+    """Two lanes' Llama-3-8B projections ([T,4096]x[4096,14336]-class) at the same time."""
+    torch.manual_seed(0)
+    T = 2048
+    xs = [torch.randn(T, 4096, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+    ws = [torch.randn(14336, 4096, device=DEV, dtype=torch.bfloat16) * 0.02,
+          torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16) * 0.02]
+    ref = [[x @ w.t() for w in ws] for x in xs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV) for _ in range(2)]
+    outs = [[None, None], [None, None]]
+    for it in range(4):
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                for j, w in enumerate(ws):
+                    outs[i][j] = xs[i] @ w.t()
+    torch.cuda.synchronize()
+    for i in range(2):
+        for j in range(2):
+            assert torch.equal(outs[i][j], ref[i][j])
