@@ -37,6 +37,9 @@ class FLConfig:
     test_samples: int = 60              # per client (local eval)
     global_test_samples: int = 100      # global eval draw (reference load_data(): 100)
     global_test_stratified: bool = True  # class-balanced global draw (majority rate = 1/C)
+    global_eval_batch: int = 256        # rows per global-eval forward (accuracy and per-example
+                                        # loss do not depend on it; local eval keeps batch_size
+                                        # for the reference's sum-of-batch-means loss quirk)
     dirichlet_alpha: float = 0.5
     resample_each_round: bool = False   # reference IID scripts draw a fresh random sample every round
     synthetic_signal: Optional[float] = None  # planted class tokens per 64 (None = generator default)

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // torch bindings of the bcfl gfx950 kernels (module bcfl._C).
 //
 // Only tensor plumbing lives here: shape/dtype checks, output allocation on the caller's stream,
@@ -447,6 +448,75 @@ Tensor sha256_merkle(Tensor leaves) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
+// Dense-layer GEMMs with fused epilogues (linear.hip). x / g rows may be strided views.
+namespace {
+int linear_tile_override() {  // BCFL_LINEAR_TILE=0|1 pins the tile config (A/B benchmarking)
+  const char* e = std::getenv("BCFL_LINEAR_TILE");
+  return e && *e ? std::atoi(e) : -1;
+}
+
+void check_gemm_operand(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.dim() == 2 && t.scalar_type() == at::kBFloat16, name, ": 2-D bf16 required");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0, name, ": 16-byte aligned contiguous rows");
+}
+}  // namespace
+
+// y[M, N] = x[M, K] w[N, K]^T (+ bias); act >= 0: returns {act(pre), pre} with pre = x w^T + b
+std::vector<Tensor> linear_fwd(Tensor x, Tensor w, optional<Tensor> bias, int64_t act) {
+  check_gemm_operand(x, "x");
+  check_gemm_operand(w, "w");
+  TORCH_CHECK(x.size(1) == w.size(1), "linear_fwd: x [M,K], w [N,K]");
+  const int M = x.size(0), N = w.size(0), K = x.size(1);
+  auto out = torch::empty({M, N}, x.options());
+  bcfl::LinearParams p{x.data_ptr(), w.data_ptr(), out.data_ptr(), x.stride(0), w.stride(0), N,
+                       M, N, K};
+  const bool hb = bias.has_value() && bias->defined();
+  if (hb) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N && bias->scalar_type() == at::kBFloat16,
+                "linear_fwd: bias [N] bf16");
+    p.bias = bias->data_ptr();
+  }
+  Tensor pre;
+  if (act >= 0) {
+    pre = torch::empty({M, N}, x.options());
+    p.epi = bcfl::EPI_BIAS_ACT;
+    p.act = (int)act;
+    p.aux = pre.data_ptr();
+    p.ldaux = N;
+  } else {
+    p.epi = hb ? bcfl::EPI_BIAS : bcfl::EPI_STORE;
+  }
+  p.tile = linear_tile_override();
+  check_rc(bcfl::launch_linear_nt(p, stream()), "linear_fwd");
+  if (act >= 0) return {out, pre};
+  return {out};
+}
+
+// dx[M, K] = g[M, N] w[N, K]; with pre (act >= 0): dx *= act'(pre) (pre [M, K], contiguous)
+Tensor linear_dgrad(Tensor g, Tensor w, optional<Tensor> pre, int64_t act) {
+  check_gemm_operand(g, "g");
+  check_gemm_operand(w, "w");
+  TORCH_CHECK(g.size(1) == w.size(0), "linear_dgrad: g [M,N], w [N,K]");
+  const int M = g.size(0), N = w.size(0), K = w.size(1);
+  auto out = torch::empty({M, K}, g.options());
+  // C[M, K] = A[M, N] B[N, K]: reduction over N
+  bcfl::LinearParams p{g.data_ptr(), w.data_ptr(), out.data_ptr(), g.stride(0), w.stride(0), K,
+                       M, K, N};
+  if (pre.has_value() && pre->defined()) {
+    TORCH_CHECK(act >= 0 && pre->is_contiguous() && pre->size(0) == M && pre->size(1) == K &&
+                pre->scalar_type() == at::kBFloat16, "linear_dgrad: pre [M,K] bf16 + act");
+    p.epi = bcfl::EPI_DACT;
+    p.act = (int)act;
+    p.aux = pre->data_ptr();
+    p.ldaux = K;
+  }
+  p.tile = linear_tile_override();
+  check_rc(bcfl::launch_linear_nn(p, stream()), "linear_dgrad");
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------------
 // dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
 std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   TORCH_CHECK(g.is_cuda() && x.is_cuda(), "wgrad: GPU tensors required");
@@ -487,6 +557,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("wgrad", &wgrad);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_dgrad", &linear_dgrad);
   m.def("wgrad_bias", &wgrad_bias);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -11,6 +11,7 @@
 //
 // All kernels use 4-wide vector accesses (8 B bf16 / 16 B fp32 per lane) and grid-stride loops
 // sized to the CU count (Guideline 11: ≤ 8 blocks per CU resident, rest grid-strided).
+#include "act.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -22,38 +23,6 @@ constexpr int EW_THREADS = 256;
 inline int ew_grid(int64_t nvec) {
   int64_t g = (nvec + EW_THREADS - 1) / EW_THREADS;
   return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
-}
-
-enum Act { ACT_GELU = 0, ACT_GELU_TANH = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4 };
-
-__device__ __forceinline__ float act_f(float x, int act) {
-  switch (act) {
-    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
-    case ACT_GELU_TANH: {
-      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-      return 0.5f * x * (1.f + tanhf(u));
-    }
-    case ACT_RELU: return x > 0.f ? x : 0.f;
-    case ACT_TANH: return tanhf(x);
-    default: return x / (1.f + __expf(-x));
-  }
-}
-
-__device__ __forceinline__ float act_d(float x, int act) {
-  switch (act) {
-    case ACT_GELU:
-      return 0.5f * (1.f + erff(x * 0.70710678118654752f)) +
-             x * 0.3989422804014327f * __expf(-0.5f * x * x);
-    case ACT_GELU_TANH: {
-      const float k = 0.7978845608028654f;
-      const float u = k * (x + 0.044715f * x * x * x);
-      const float t = tanhf(u);
-      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
-    }
-    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
-    case ACT_TANH: { const float t = tanhf(x); return 1.f - t * t; }
-    default: { const float sg = 1.f / (1.f + __expf(-x)); return sg * (1.f + x * (1.f - sg)); }
-  }
 }
 
 // 2-D launch for row-structured elementwise kernels: grid.x covers the columns in 8-element

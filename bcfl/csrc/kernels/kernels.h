@@ -89,6 +89,24 @@ struct WgradParams {
 int wgrad_splits(int M, int N, int K, int* Mc);
 int launch_wgrad(const WgradParams& p, hipStream_t s);
 
+// ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
+enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3 };
+struct LinearParams {
+  const void* A;       // [M, K] bf16, row stride lda
+  const void* B;       // NT: [N, K] (ldb);  NN: [K, N] (ldb)
+  void* C;             // [M, N] bf16, row stride ldc
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int epi = EPI_STORE;
+  int act = 0;                   // activation id (act.h) for EPI_BIAS_ACT / EPI_DACT
+  const void* bias = nullptr;    // [N] bf16 (EPI_BIAS / EPI_BIAS_ACT)
+  void* aux = nullptr;           // [M, N] bf16 pre-activation: written by EPI_BIAS_ACT, read by EPI_DACT
+  int64_t ldaux = 0;
+  int tile = -1;                 // -1 auto | 0: 128 x 128 (4 waves) | 1: 256 x 256 (8 waves)
+};
+int launch_linear_nt(const LinearParams& p, hipStream_t s);  // C = A B^T
+int launch_linear_nn(const LinearParams& p, hipStream_t s);  // C = A B
+
 // ---- attention.hip -----------------------------------------------------------------------------
 struct AttnParams {
   const void* qkv;     // [T, (nh + 2 nkv) * d] bf16

@@ -414,10 +414,26 @@ class Federation:
                           seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple)
         return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
 
+    def _cached_batches(self, key, build):
+        """Evaluation batches are a pure function of the (per-round when resampling) draw: build
+        and upload them once, keep them resident on the device (read-only afterwards)."""
+        if not hasattr(self, "_batch_cache"):
+            self._batch_cache = {}
+        if key not in self._batch_cache:
+            if len(self._batch_cache) > 4 * (self.cfg.num_clients + 1):
+                self._batch_cache.clear()  # resampling draws: keep only recent rounds
+            self._batch_cache[key] = build()
+        return self._batch_cache[key]
+
+    def _draw_key(self, r: int) -> int:
+        return r if self.cfg.resample_each_round else 0
+
     def test_batches(self, c: int, r: int):
         sp = self.partitions(r)[c]
-        return ClientLoader(self.test_ds, sp.test, self.cfg.batch_size,
-                            pad_multiple=self.pad_multiple).device_batches(self.device)
+        return self._cached_batches(
+            ("test", c, self._draw_key(r)),
+            lambda: ClientLoader(self.test_ds, sp.test, self.cfg.batch_size,
+                                 pad_multiple=self.pad_multiple).device_batches(self.device))
 
     def global_test_idx(self, r: int) -> np.ndarray:
         c = self.cfg
@@ -436,8 +452,10 @@ class Federation:
         mine = idx if self.collective_free else idx[self.rt.rank::self.rt.world]
         if len(mine) == 0:
             return []
-        return ClientLoader(self.test_ds, mine, self.cfg.batch_size,
-                            pad_multiple=self.pad_multiple).device_batches(self.device)
+        return self._cached_batches(
+            ("global", self._draw_key(r)),
+            lambda: ClientLoader(self.test_ds, mine, max(self.cfg.global_eval_batch, 1),
+                                 pad_multiple=self.pad_multiple).device_batches(self.device))
 
     def _activate(self, c: int, master: Optional[torch.Tensor] = None):
         if master is not None:

@@ -100,8 +100,9 @@ class AlbertForSequenceClassification(SeqClassifierBase):
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.dense_weight), self.dense_bias, x,
                                             self.attn_ln_weight, self.attn_ln_bias,
                                             c.layer_norm_eps, c.hidden_dropout_prob, tr)
-        h = ops.bias_act(ops.linear(x1, self.ffn_weight), self.ffn_bias, c.hidden_act)
-        return ops.bias_dropout_add_layernorm(ops.linear(h, self.ffn_out_weight), self.ffn_out_bias,
+        h, pre = ops.linear_act(x1, self.ffn_weight, self.ffn_bias, c.hidden_act)
+        y2 = ops.linear_after_act(h, pre, self.ffn_out_weight, c.hidden_act)
+        return ops.bias_dropout_add_layernorm(y2, self.ffn_out_bias,
                                               x1, self.full_ln_weight, self.full_ln_bias,
                                               c.layer_norm_eps, 0.0, tr)
 

@@ -89,8 +89,9 @@ class BertLayer(nn.Module):
         x1 = ops.bias_dropout_add_layernorm(y, self.attn_out_bias, x, self.attn_ln_weight,
                                             self.attn_ln_bias, c.layer_norm_eps,
                                             c.hidden_dropout_prob, tr)
-        h = ops.bias_act(ops.linear(x1, self.inter_weight), self.inter_bias, c.hidden_act)
-        y2 = ops.linear(h, self.out_weight)
+        # dense -> GELU in one GEMM epilogue; the output GEMM's backward applies GELU' (K6)
+        h, pre = ops.linear_act(x1, self.inter_weight, self.inter_bias, c.hidden_act)
+        y2 = ops.linear_after_act(h, pre, self.out_weight, c.hidden_act)
         return ops.bias_dropout_add_layernorm(y2, self.out_bias, x1, self.out_ln_weight,
                                               self.out_ln_bias, c.layer_norm_eps,
                                               c.hidden_dropout_prob, tr)

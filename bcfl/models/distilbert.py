@@ -73,8 +73,9 @@ class DistilBertLayer(nn.Module):
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.out_lin_weight), self.out_lin_bias,
                                             x, self.sa_ln_weight, self.sa_ln_bias,
                                             c.layer_norm_eps, 0.0, tr)
-        h = ops.bias_act(ops.linear(x1, self.lin1_weight), self.lin1_bias, c.activation)
-        return ops.bias_dropout_add_layernorm(ops.linear(h, self.lin2_weight), self.lin2_bias, x1,
+        h, pre = ops.linear_act(x1, self.lin1_weight, self.lin1_bias, c.activation)
+        y2 = ops.linear_after_act(h, pre, self.lin2_weight, c.activation)
+        return ops.bias_dropout_add_layernorm(y2, self.lin2_bias, x1,
                                               self.out_ln_weight, self.out_ln_bias,
                                               c.layer_norm_eps, c.dropout, tr)
 

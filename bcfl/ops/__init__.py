@@ -4,7 +4,8 @@ from ._native import available as native_available, native, use_native, load_err
 from .functional import (bias_dropout_add_layernorm, layernorm, bias_act, varlen_attention,
                          query_subset_attention,
                          embedding_layernorm, rmsnorm, rope, swiglu, cross_entropy, linear, dropout,
-                         wgrad, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad)
+                         wgrad, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad, linear_act,
+                         linear_after_act, gemm_supported)
 from .flat import (adamw_, adamw_multi_, gossip_mix_, weighted_accumulate_, block_sketch, scale_, axpby_,
                    cast_copy_, merkle_root_sha256, merkle_root_deferred, root_bytes,
                    leaf_digests_sha256)
@@ -13,7 +14,8 @@ __all__ = [
     "rng", "ref", "native_available", "native", "use_native", "load_error",
     "bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention", "query_subset_attention",
     "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "dropout", "wgrad",
-    "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad",
+    "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad", "linear_act", "linear_after_act",
+    "gemm_supported",
     "adamw_", "adamw_multi_", "gossip_mix_", "weighted_accumulate_", "block_sketch", "scale_", "axpby_",
     "cast_copy_", "merkle_root_sha256", "merkle_root_deferred", "root_bytes", "leaf_digests_sha256",
 ]

@@ -13,6 +13,7 @@ Hot-path ops (SURVEY.md §2.6 device-op inventory K1–K11):
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -23,6 +24,7 @@ from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
+           "linear_act", "linear_after_act", "gemm_supported",
            "query_subset_attention", "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
@@ -105,10 +107,66 @@ def _wgrad_async(g2, x2, want_b):
     return dw, db
 
 
+# Plain (epilogue-free) forward / input-gradient GEMMs go to hipBLASLt by default: on the bench
+# shapes (K = 768 / 3072, 12-48 reduction steps) it is 1.2-1.4x faster than linear.hip's
+# register-staged tiles in isolation and equal inside the 8-lane bench
+# (profiles/linear_gemm_vs_hipblaslt.md). The fused-epilogue GEMMs (bias+GELU forward, GELU'
+# dgrad) always run on linear.hip — that fusion is what the library cannot do (K6).
+# BCFL_GEMM_PLAIN=1 routes the plain GEMMs to linear.hip as well.
+_GEMM_PLAIN_NATIVE = os.environ.get("BCFL_GEMM_PLAIN", "0") == "1"
+
+
+def gemm_supported(x2: torch.Tensor, w: torch.Tensor, nn_: bool = False, op: str = "gemm") -> bool:
+    """Shapes the linear.hip MFMA kernels take: bf16, 16-byte aligned contiguous rows, output
+    features a multiple of 128 and reduction a multiple of 64 (``nn_``: the dgrad GEMM, whose
+    output is the weight's input dim)."""
+    if op == "gemm" and not _GEMM_PLAIN_NATIVE:
+        return False
+    out_f, in_f = w.shape
+    n, k = (in_f, out_f) if nn_ else (out_f, in_f)
+    return (x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and n % 128 == 0
+            and k % 64 == 0 and x2.stride(-1) == 1 and x2.stride(0) % 8 == 0
+            and w.is_contiguous() and use_native(x2, op))
+
+
+def _fwd_gemm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    x2 = x.reshape(-1, x.shape[-1])
+    if gemm_supported(x2, w):
+        return native().linear_fwd(x2, w, b, -1)[0].view(*x.shape[:-1], w.shape[0])
+    return torch.nn.functional.linear(x, w, b)
+
+
+def _dgrad_gemm(g2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if gemm_supported(g2, w, nn_=True):
+        return native().linear_dgrad(g2, w, None, -1)
+    return g2.mm(w)
+
+
+def _weight_grads(ctx, g2, x2, w, bias, need_w: bool, want_b: bool):
+    """(dW, db) for y = x W^T + b: K9 split-M MFMA kernel (bias gradient fused in), optionally on
+    the side stream (overlap) when AccumulateGrad will steal the result."""
+    dw = db = None
+    # The side-stream dW is only safe when AccumulateGrad STEALS it (no .grad yet): if a
+    # gradient is already there, autograd adds into it on its own stream, reading dW before
+    # the side-stream kernel finished -> compute it inline instead.
+    steal = w.grad is None and (bias is None or bias.grad is None)
+    if (need_w and _WG["enabled"] and not ctx.shared and steal and use_native(g2)
+            and wgrad_supported(g2, x2)):
+        dw, db = _wgrad_async(g2, x2, want_b)
+    elif need_w:
+        if want_b and use_native(g2) and wgrad_supported(g2, x2):
+            dw, db = native().wgrad_bias(g2, x2)  # bias gradient fused into the K9 kernel
+        else:
+            dw = wgrad(g2, x2)
+    if want_b and db is None:
+        db = g2.sum(0)
+    return dw, db
+
+
 class _Linear(torch.autograd.Function):
-    """y = x W^T (+ b). Forward and input-gradient GEMMs are hipBLASLt (they run at 560-820 TF/s
-    on the BERT shapes); the weight gradient — long reduction over tokens, small output — goes
-    to the split-M MFMA kernel (gemm.hip), optionally on a side stream (overlap)."""
+    """y = x W^T (+ b). Forward / input-gradient GEMMs: linear.hip (MFMA, bias fused into the
+    epilogue) where the shape allows, else the library; weight gradient: the split-M K9 kernel
+    (gemm.hip), optionally on a side stream (overlap)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -118,7 +176,7 @@ class _Linear(torch.autograd.Function):
         # autograd's stream, which a side-stream dW would race with
         ctx.shared = getattr(w, "_bcfl_shared", False) or getattr(b, "_bcfl_shared", False)
         ctx.bias = b
-        return torch.nn.functional.linear(x, w, b)
+        return _fwd_gemm(x, w, b)
 
     @staticmethod
     def backward(ctx, g):
@@ -126,38 +184,109 @@ class _Linear(torch.autograd.Function):
         N, K = w.shape
         g2 = g.reshape(-1, N)
         x2 = x.reshape(-1, K)
-        dx = dw = db = None
+        dx = None
         if ctx.needs_input_grad[0]:
-            dx = g2.mm(w).view(x.shape)
+            dx = _dgrad_gemm(g2, w).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        # The side-stream dW is only safe when AccumulateGrad STEALS it (no .grad yet): if a
-        # gradient is already there, autograd adds into it on its own stream, reading dW before
-        # the side-stream kernel finished -> compute it inline instead.
-        steal = w.grad is None and (ctx.bias is None or ctx.bias.grad is None)
-        if (ctx.needs_input_grad[1] and _WG["enabled"] and not ctx.shared and steal
-                and use_native(g2) and wgrad_supported(g2, x2)):
-            dw, db = _wgrad_async(g2, x2, want_b)
-        elif ctx.needs_input_grad[1]:
-            if want_b and use_native(g2) and wgrad_supported(g2, x2):
-                dw, db = native().wgrad_bias(g2, x2)  # bias gradient fused into the K9 kernel
-            else:
-                dw = wgrad(g2, x2)
-        if want_b and db is None:
-            db = g2.sum(0)
+        dw, db = _weight_grads(ctx, g2, x2, w, ctx.bias, ctx.needs_input_grad[1], want_b)
         return dx, dw, db
 
 
+class _LinearAct(torch.autograd.Function):
+    """(h, pre) with pre = x W^T + b and h = act(pre), in ONE GEMM (EPI_BIAS_ACT epilogue).
+    ``pre`` carries the gradient: the NEXT layer (:class:`_LinearAfterAct`) returns dL/dpre
+    directly (its dgrad epilogue applies act'), so this backward is dgrad + wgrad only — the
+    bias+activation forward and backward passes over [T, I] disappear (K6)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act_id):
+        x2 = x.reshape(-1, x.shape[-1])
+        h, pre = native().linear_fwd(x2, w, b, int(act_id))
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        ctx.shared = getattr(w, "_bcfl_shared", False) or getattr(b, "_bcfl_shared", False)
+        ctx.bias = b
+        ctx.mark_non_differentiable(h)
+        shp = (*x.shape[:-1], w.shape[0])
+        return h.view(shp), pre.view(shp)
+
+    @staticmethod
+    def backward(ctx, _dh, dpre):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        g2 = dpre.reshape(-1, N)
+        x2 = x.reshape(-1, K)
+        dx = _dgrad_gemm(g2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        dw, db = _weight_grads(ctx, g2, x2, w, ctx.bias, ctx.needs_input_grad[1], want_b)
+        return dx, dw, db, None
+
+
+class _LinearAfterAct(torch.autograd.Function):
+    """y = h W^T where h = act(pre) came from :class:`_LinearAct`; backward returns the gradient
+    w.r.t. ``pre``: dgrad GEMM with the EPI_DACT epilogue (dh * act'(pre) in the same kernel)."""
+
+    @staticmethod
+    def forward(ctx, h, pre, w, act_id):
+        ctx.save_for_backward(h, pre, w)
+        ctx.act_id = int(act_id)
+        ctx.shared = getattr(w, "_bcfl_shared", False)
+        ctx.bias = None
+        return _fwd_gemm(h, w, None)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, pre, w = ctx.saved_tensors
+        N, K = w.shape
+        g2 = g.reshape(-1, N)
+        h2 = h.reshape(-1, K)
+        dpre = None
+        if ctx.needs_input_grad[1]:
+            dpre = native().linear_dgrad(g2, w, pre.reshape(-1, K), ctx.act_id).view(pre.shape)
+        dw, _ = _weight_grads(ctx, g2, h2, w, None, ctx.needs_input_grad[2], False)
+        return None, dpre, dw, None
+
+
 def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (use_native(x) and w.requires_grad and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+    return (use_native(x) and (w.requires_grad or x.requires_grad) and torch.is_grad_enabled()
+            and x.dtype == torch.bfloat16
             and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0 and x.numel() // w.shape[1] >= WGRAD_MIN_ROWS)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Dense layer. GPU + bf16 + a weight that trains: :class:`_Linear` (library fwd/dgrad GEMMs,
-    hand-written K9 wgrad); otherwise the plain library GEMM."""
+    """Dense layer. GPU + bf16 + a weight that trains: :class:`_Linear` (linear.hip fwd/dgrad
+    GEMMs, K9 wgrad); frozen / inference: the fused-epilogue forward GEMM alone; otherwise the
+    plain library GEMM."""
     if _use_linear_fn(x, w):
         return _Linear.apply(x, w, b)
+    if use_native(x) and not (torch.is_grad_enabled() and (w.requires_grad or x.requires_grad)):
+        return _fwd_gemm(x, w, b)
     return torch.nn.functional.linear(x, w, b)
+
+
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "gelu"):
+    """(h, pre): h = act(x W^T + b). On the GPU fast path both come out of ONE GEMM and ``pre``
+    must be handed to :func:`linear_after_act` (which routes the gradient); elsewhere ``pre`` is
+    None and h is an ordinary autograd tensor."""
+    aid = _ACT_ID[act]
+    x2 = x.reshape(-1, x.shape[-1])
+    if aid in (0, 1, 2) and (_use_linear_fn(x, w) or (use_native(x) and not torch.is_grad_enabled())) and \
+            gemm_supported(x2, w, op="gemm_act"):
+        if not torch.is_grad_enabled():
+            h, _ = native().linear_fwd(x2, w, b, aid)
+            return h.view(*x.shape[:-1], w.shape[0]), None
+        return _LinearAct.apply(x, w, b, aid)
+    return bias_act(linear(x, w), b, act), None
+
+
+def linear_after_act(h: torch.Tensor, pre: Optional[torch.Tensor], w: torch.Tensor,
+                     act: str = "gelu") -> torch.Tensor:
+    """y = h W^T for h from :func:`linear_act` (gradient routed to ``pre`` when given)."""
+    if pre is not None and torch.is_grad_enabled() and pre.requires_grad:
+        h2 = h.reshape(-1, h.shape[-1])
+        if gemm_supported(h2, w, op="gemm_act") and gemm_supported(h2, w, nn_=True, op="gemm_act"):
+            return _LinearAfterAct.apply(h, pre, w, _ACT_ID[act])
+    return linear(h, w)
 
 
 # ----------------------------------------------------------------------------------------

@@ -373,3 +373,87 @@ def test_overlapped_wgrad_matches_inline(model):
     assert len(grads[False]) == len(grads[True])
     for a, c in zip(grads[False], grads[True]):
         assert torch.equal(a, c)
+
+
+# ---------------------------------------------------------------------------------------------
+# linear.hip: dense-layer GEMMs with fused epilogues vs fp32 references
+_LIN_SHAPES = [(11264, 768, 768), (1000, 2304, 768), (333, 3072, 768), (2048, 768, 3072),
+               (1088, 4096, 4096), (64, 128, 64)]
+
+
+@pytest.fixture(params=["0", "1"], ids=["tile128", "tile256"])
+def lin_tile(request, monkeypatch):
+    monkeypatch.setenv("BCFL_LINEAR_TILE", request.param)
+    return int(request.param)
+
+
+@pytest.mark.parametrize("M,N,K", _LIN_SHAPES)
+@pytest.mark.parametrize("epi", ["store", "bias", "gelu", "gelu_new"])
+def test_linear_fwd_epilogues(M, N, K, epi, lin_tile):
+    torch.manual_seed(0)
+    C = ops.native()
+    xs = torch.randn(M, K + 64, device=DEV).bfloat16()
+    x = xs[:, :K]  # strided rows (ld = K + 64)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16() if epi != "store" else None
+    act = {"store": -1, "bias": -1, "gelu": 0, "gelu_new": 1}[epi]
+    out = C.linear_fwd(x, w, b, act)
+    ref = x.float() @ w.float().t() + (b.float() if b is not None else 0)
+    if act < 0:
+        _close(out[0], ref, 2e-2, 2e-2)
+    else:
+        h, pre = out
+        _close(pre, ref, 2e-2, 2e-2)
+        fn = torch.nn.functional.gelu
+        _close(h, fn(pre.float(), approximate="none" if act == 0 else "tanh"), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", _LIN_SHAPES)
+@pytest.mark.parametrize("with_act", [False, True])
+def test_linear_dgrad(M, N, K, with_act, lin_tile):
+    """dx[M, K] = g[M, N] W[N, K] (NN: hardware-transposed W tiles), optionally * gelu'(pre)."""
+    if K % 128:
+        pytest.skip("dgrad output dim must be a multiple of 128 (library GEMM otherwise)")
+    torch.manual_seed(1)
+    C = ops.native()
+    g = torch.randn(M, N, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * N ** -0.5).bfloat16()
+    pre = torch.randn(M, K, device=DEV).bfloat16() if with_act else None
+    dx = C.linear_dgrad(g, w, pre, 0 if with_act else -1)
+    ref = g.float() @ w.float()
+    if with_act:
+        p = pre.float().requires_grad_(True)
+        torch.nn.functional.gelu(p).backward(ref)
+        ref = p.grad
+    _close(dx, ref, 2e-2, 2e-2)
+
+
+def test_fused_ffn_autograd_matches_reference():
+    """linear_act + linear_after_act (GEMM epilogues carry bias+GELU and GELU') == the unfused
+    library path, forward and every gradient."""
+    import os
+    torch.manual_seed(2)
+    T, H, I = 2048, 768, 3072
+    x0 = torch.randn(T, H, device=DEV).bfloat16()
+    w1 = (torch.randn(I, H, device=DEV) * 0.02).bfloat16()
+    b1 = (torch.randn(I, device=DEV) * 0.1).bfloat16()
+    w2 = (torch.randn(H, I, device=DEV) * 0.02).bfloat16()
+    gy = torch.randn(T, H, device=DEV).bfloat16()
+    res = {}
+    for route in ("bcfl", "torch"):
+        os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "gemm,gemm_act"
+        try:
+            x = x0.clone().requires_grad_(True)
+            p1, q1, p2 = (t.clone().requires_grad_(True) for t in (w1, b1, w2))
+            h, pre = ops.linear_act(x, p1, q1, "gelu")
+            assert (pre is not None) == (route == "bcfl")
+            y = ops.linear_after_act(h, pre, p2, "gelu")
+            y.backward(gy)
+            res[route] = [y, x.grad, p1.grad, q1.grad, p2.grad]
+        finally:
+            os.environ["BCFL_TORCH_OPS"] = ""
+    for name, a, b in zip(("y", "dx", "dW1", "db1", "dW2"), res["bcfl"], res["torch"]):
+        # both sides are bf16 results of fp32 accumulations with different rounding points
+        # (fused epilogue vs bf16 GEMM output + separate bias/GELU): compare normwise
+        err = ((a.float() - b.float()).norm() / b.float().norm()).item()
+        assert err < 1e-2, (name, err)
