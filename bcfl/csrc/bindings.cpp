@@ -153,13 +153,21 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor cu, int64_t max_s, int64_t nh, i
   p.scale = (float)scale;
   p.causal = causal;
   p.p8 = (uint32_t)p8; p.ka = (uint32_t)ka; p.kb = (uint32_t)kb;
+  // dropout: the forward writes its keep decisions as a bitmask the backward kernels reuse
+  Tensor mask = torch::empty({0}, qkv.options().dtype(torch::kInt));
+  if (p8 > 0 && T > 0) {
+    const int W = bcfl::attn_dropmask_words((int)max_s);
+    mask = torch::empty({(int64_t)T * nh * W}, qkv.options().dtype(torch::kInt));
+    p.mask = reinterpret_cast<uint32_t*>(mask.data_ptr<int>());
+    p.mask_w = W;
+  }
   if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_fwd(p, stream()), "attn_fwd");
-  return {out, lse};
+  return {out, lse, mask};
 }
 
 Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int64_t max_s,
                 int64_t nh, int64_t nkv, int64_t d, double scale, bool causal, int64_t p8,
-                int64_t ka, int64_t kb) {
+                int64_t ka, int64_t kb, Tensor mask) {
   check_cuda(dout, "dout");
   check_cuda(qkv, "qkv");
   check_cuda(out, "out");
@@ -181,6 +189,13 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
   p.scale = (float)scale;
   p.causal = causal;
   p.p8 = (uint32_t)p8; p.ka = (uint32_t)ka; p.kb = (uint32_t)kb;
+  if (p8 > 0 && T > 0) {
+    const int W = bcfl::attn_dropmask_words((int)max_s);
+    TORCH_CHECK(mask.is_cuda() && mask.numel() == (int64_t)T * nh * W,
+                "attn_bwd: dropout keep bitmask from attn_fwd required");
+    p.mask = reinterpret_cast<const uint32_t*>(mask.data_ptr<int>());
+    p.mask_w = W;
+  }
   if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_bwd(p, stream()), "attn_bwd");
   return dqkv;
 }

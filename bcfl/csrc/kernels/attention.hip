@@ -29,6 +29,11 @@
 // Softmax VALU trims (d = 64 makes attention VALU-heavy): the softmax scale is folded into the
 // exp2 FMA (max taken on raw scores), key masking runs only on tiles that straddle the sequence
 // end / causal diagonal, and the O rescale is skipped unless some row's running max grew.
+//
+// Dropout keep bits: the forward evaluates the counter hash (bcfl/ops/rng.py layout, one hash per
+// 4 scores) and also WRITES the decisions as a bitmask (1 bit per score, ~6 MB per BERT layer);
+// the dq and dkdv kernels read those bits back — 2 VALU ops per score (bit-field extract to a
+// 0 / -1 mask + AND) instead of re-hashing in each of them.
 #include <math.h>
 
 #include "common.h"
@@ -54,6 +59,11 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 template <int E>
 __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, E | (E << 2) | (E << 4) | (E << 6), 0xf, 0xf, false);
+}
+
+// 0 or -1 (all ones) from bit `pos` of w: AND it into a float's bits to apply a keep decision
+__device__ __forceinline__ float keep_and(float v, uint32_t w, int pos) {
+  return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe((int)w, pos, 1));
 }
 
 // Register-staged loader of two [TILE x HD] row tiles (e.g. K and V) gathered from token rows
@@ -131,6 +141,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
   const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
   const int myq = qw0 + r;
   const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
+  // this lane's keep-bit row (query clamped into the sequence: rows past L are never read)
+  uint32_t* mrow = p.mask + (size_t)((tok0 + min(myq, L - 1)) * p.nh + h) * p.mask_w;
 
   TileOffsets<HD> to;
   to.init(lane);
@@ -181,7 +193,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
       bf16x8_t pf[4];
       float ls = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        // lane-half hh holds keys acc_row(reg, hh) = (reg & 3) + 8 (reg >> 2) + 4 hh of the block
+        uint32_t bits = 0;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           uint32_t hsh = 0;
@@ -191,10 +205,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
             const int reg = 4 * g4 + e;
             float pv = fexp2(fmaf(sacc[t][reg], sl2, -m));
             ls += pv;
-            if (p.p8) pv = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? pv : 0.f;  // 1/(1-p) applied at the end
+            if (p.p8) {
+              const bool keep = ((hsh >> (8 * e)) & 0xffu) >= p.p8;
+              bits |= (keep ? 1u : 0u) << (e + 8 * g4);
+              pv = keep ? pv : 0.f;  // 1/(1-p) applied at the end
+            }
             pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
           }
         }
+        if (p.p8) {  // publish the 32 decisions of this (query, key block) for the backward
+          bits <<= 4 * hh;
+          bits |= __shfl_xor(bits, 32, 64);
+          if (hh == t && myq < L) mrow[(k0 >> 5) + t] = bits;  // clamped rows alias row L-1
+        }
+      }
       l += ls;
 #pragma unroll
       for (int u = 0; u < HD / 32; ++u)
@@ -297,7 +321,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) dq[u] = zero16();
   const float sl2 = p.scale * LOG2E;
-  const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
+  const uint32_t* mrow = p.mask + (size_t)((tok0 + qi) * p.nh + h) * p.mask_w;
 
   TileOffsets<HD> to;
   to.init(lane);
@@ -308,6 +332,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
     const int k0 = it * TILE;
     const bool more = it + 1 < ntiles;
     if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);
+    uint2 kw2 = make_uint2(0u, 0u);
+    if (p.p8) kw2 = *reinterpret_cast<const uint2*>(mrow + (k0 >> 5));
     const bf16_t* Ks = lds + (it & 1) * STG;
     const bf16_t* Vs = Ks + TILE * HD;
     if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
@@ -325,24 +351,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
       const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
       bf16x8_t dsf[4];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t wk = (t ? kw2.y : kw2.x) >> (4 * hh);
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          uint32_t hsh = 0;
-          if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int reg = 4 * g4 + e;
-            float pv = fexp2(fmaf(sacc[t][reg], sl2, -lse2));
-            if (need_mask) {
-              const int key = k0 + 32 * t + acc_row(reg, hh);
-              if (key >= L || (p.causal && key > myq)) pv = 0.f;
-            }
-            float dp = pacc[t][reg];
-            if (p.p8) dp = (((hsh >> (8 * e)) & 0xffu) >= p.p8) ? dp : 0.f;
-            dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
+        for (int reg = 0; reg < 16; ++reg) {
+          float pv = fexp2(fmaf(sacc[t][reg], sl2, -lse2));
+          if (need_mask) {
+            const int key = k0 + 32 * t + acc_row(reg, hh);
+            if (key >= L || (p.causal && key > myq)) pv = 0.f;
           }
+          float dp = pacc[t][reg];
+          if (p.p8) dp = keep_and(dp, wk, (reg & 3) + 8 * (reg >> 2));
+          dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
         }
+      }
 #pragma unroll
       for (int u = 0; u < HD / 32; ++u)
 #pragma unroll
@@ -370,7 +392,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 // ------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
-  constexpr int STG = 2 * TILE * HD + 2 * TILE * 2;  // Q | dO | lse, delta (fp32 = 2 bf16 slots)
+  // Q | dO | lse, delta (fp32 = 2 bf16 slots) | keep words [4 waves][64 queries] (uint32)
+  constexpr int STG = 2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
@@ -399,6 +422,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   const float lsd = log2f(sd), isd = 1.f / sd;
   Stage2<HD> stg;
   float ls_r = 0.f, dl_r = 0.f;  // lse / delta of row threadIdx.x (threads < TILE)
+  uint32_t mk_r = 0u;            // keep word: wave (threadIdx.x >> 6)'s key block, query tid & 63
   auto issue = [&](int it) {
     const int hq = hk * grp + it / nqt;
     const int q0 = qstart + (it % nqt) * TILE;
@@ -407,6 +431,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
       const int q = q0 + threadIdx.x;
       ls_r = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E - lsd : 0.f;
       dl_r = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] * isd : 0.f;
+    }
+    if (p.p8) {
+      const int q = q0 + (threadIdx.x & 63);
+      mk_r = q < L ? p.mask[(size_t)((tok0 + q) * p.nh + hq) * p.mask_w + (kb0 >> 5) + (threadIdx.x >> 6)]
+                   : 0u;
     }
   };
   auto commit = [&](int buf) {
@@ -418,6 +447,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
       fs[threadIdx.x] = ls_r;
       fs[TILE + threadIdx.x] = dl_r;
     }
+    reinterpret_cast<uint32_t*>(fs + 2 * TILE)[threadIdx.x] = mk_r;
   };
   issue(0);
 
@@ -434,10 +464,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv[u] = zero16(); }
   const float sl2 = p.scale * LOG2E;
-  // dropout keep bits: element (q, key) uses byte key&3 of hash((q*nh+hq)*2048 + key/4); the 4
-  // lanes of a quad (keys 4j..4j+3) share those hashes, so lane j of the quad hashes query e=j and
-  // the others receive it by DPP quad broadcast (4x fewer quarter-rate v_mul_lo_u32 chains).
-  const uint32_t kq = (uint32_t)mykey >> 2, bsh = 8u * (uint32_t)(r & 3);
 
   TileOffsets<HD> to;
   to.init(lane);
@@ -453,6 +479,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
     const bf16_t* Ds = Qs + TILE * HD;
     const float* lse_s = reinterpret_cast<const float*>(Ds + TILE * HD);
     const float* dl_s = lse_s + TILE;
+    // keep words of this wave's 32 keys (bit r = my key) for the tile's 64 queries
+    const uint32_t* mk_s = reinterpret_cast<const uint32_t*>(lse_s + 2 * TILE) + wid * TILE;
     if (active) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -473,16 +501,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
           const float4 ls4 = *reinterpret_cast<const float4*>(lse_s + ql);
           const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + ql);
           const float lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
-          uint32_t hq4[4] = {0u, 0u, 0u, 0u};
-          if (p.p8) {
-            const uint32_t mine = hash32(
-                (((uint32_t)((tok0 + q0 + ql + (r & 3)) * p.nh + hq) * (uint32_t)DROP_STRIDE) >> 2) + kq,
-                p.ka, p.kb);
-            hq4[0] = quad_bcast<0>(mine);
-            hq4[1] = quad_bcast<1>(mine);
-            hq4[2] = quad_bcast<2>(mine);
-            hq4[3] = quad_bcast<3>(mine);
-          }
+          uint4 m4 = make_uint4(0u, 0u, 0u, 0u);
+          if (p.p8) m4 = *reinterpret_cast<const uint4*>(mk_s + ql);
+          const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int reg = 4 * g4 + e;
@@ -491,9 +512,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
             if (need_mask && (q >= L || (p.causal && mykey > q))) pv = 0.f;
             float pd = pv, dp = pacc[reg];
             if (p.p8) {
-              const bool keep = ((hq4[e] >> bsh) & 0xffu) >= p.p8;
-              pd = keep ? pv : 0.f;
-              dp = keep ? dp : 0.f;
+              const int km = __builtin_amdgcn_sbfe((int)mw[e], r, 1);
+              pd = __int_as_float(__float_as_int(pv) & km);
+              dp = __int_as_float(__float_as_int(dp) & km);
             }
             pf[reg >> 3][reg & 7] = (__bf16)pd;
             dsf[reg >> 3][reg & 7] = (__bf16)(pv * (dp - dlv[e]));
@@ -546,11 +567,20 @@ void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
                      dim3(256), 0, s, dout, out, p.delta, rows);
   hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)2 * 2 * TILE * HD * 2, s, p);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, gk, dim3(256),
-                     (size_t)2 * (2 * TILE * HD + 2 * TILE * 2) * 2, s, p);
+                     (size_t)2 * (2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2) * 2, s, p);
+}
+
+int attn_dropmask_words(int max_s) {
+  // >= one word per 32 keys and >= the 4 key blocks of the last dkdv workgroup; power of two
+  const int need = 4 * ((max_s + BLK - 1) / BLK);
+  int w = 4;
+  while (w < need) w <<= 1;
+  return w;
 }
 
 int launch_attn_fwd(const AttnParams& p, hipStream_t s) {
   if (p.nh % p.nkv) return -2;
+  if (p.p8 && (!p.mask || p.mask_w < attn_dropmask_words(p.max_s))) return -3;
   switch (p.d) {
     case 32: fwd_hd<32>(p, s); break;
     case 64: fwd_hd<64>(p, s); break;
@@ -562,6 +592,7 @@ int launch_attn_fwd(const AttnParams& p, hipStream_t s) {
 
 int launch_attn_bwd(const AttnBwdParams& p, hipStream_t s) {
   if (p.nh % p.nkv) return -2;
+  if (p.p8 && (!p.mask || p.mask_w < attn_dropmask_words(p.max_s))) return -3;
   switch (p.d) {
     case 32: bwd_hd<32>(p, s); break;
     case 64: bwd_hd<64>(p, s); break;

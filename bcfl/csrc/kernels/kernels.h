@@ -117,6 +117,8 @@ struct AttnParams {
   float scale;
   int causal;
   uint32_t p8, ka, kb;
+  uint32_t* mask = nullptr;  // dropout keep bitmask [T * nh * mask_w], WRITTEN here (if p8)
+  int mask_w = 0;            // words per (token, head) row (attn_dropmask_words)
 };
 struct AttnBwdParams {
   const void* qkv;
@@ -130,7 +132,12 @@ struct AttnBwdParams {
   float scale;
   int causal;
   uint32_t p8, ka, kb;
+  const uint32_t* mask = nullptr;
+  int mask_w = 0;
 };
+// dropout keep bitmask, 1 bit per score: word (t * nh + h) * W + kw, bit j = keep(key 32 kw + j);
+// written by the forward, read by the backward kernels
+int attn_dropmask_words(int max_s);  // W
 int launch_attn_fwd(const AttnParams& p, hipStream_t s);
 int launch_attn_bwd(const AttnBwdParams& p, hipStream_t s);
 

@@ -360,19 +360,19 @@ class _VarlenAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cu, max_s, nh, nkv, d, scale, causal, p8, ka, kb):
         C = native()
-        out, lse = C.attn_fwd(qkv, cu, int(max_s), int(nh), int(nkv), int(d), float(scale),
-                              bool(causal), int(p8), int(ka), int(kb))
-        ctx.save_for_backward(qkv, cu, out, lse)
+        out, lse, mask = C.attn_fwd(qkv, cu, int(max_s), int(nh), int(nkv), int(d), float(scale),
+                                    bool(causal), int(p8), int(ka), int(kb))
+        ctx.save_for_backward(qkv, cu, out, lse, mask)
         ctx.cfg = (max_s, nh, nkv, d, scale, causal, p8, ka, kb)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, cu, out, lse = ctx.saved_tensors
+        qkv, cu, out, lse, mask = ctx.saved_tensors
         max_s, nh, nkv, d, scale, causal, p8, ka, kb = ctx.cfg
         dqkv = native().attn_bwd(dout.contiguous(), qkv, out, lse, cu, int(max_s), int(nh),
                                  int(nkv), int(d), float(scale), bool(causal), int(p8), int(ka),
-                                 int(kb))
+                                 int(kb), mask)
         return dqkv, None, None, None, None, None, None, None, None, None, None
 
 

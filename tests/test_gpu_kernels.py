@@ -116,7 +116,7 @@ def test_attention_lse():
     lens = [100, 37]
     cu = np.array([0, 100, 137], dtype=np.int32)
     qkv = torch.randn(137, 3 * 4 * 64, device=DEV).bfloat16()
-    out, lse = ops.native().attn_fwd(qkv, torch.from_numpy(cu).to(DEV), 100, 4, 4, 64, 0.125, False, 0, 0, 0)
+    out, lse, _ = ops.native().attn_fwd(qkv, torch.from_numpy(cu).to(DEV), 100, 4, 4, 64, 0.125, False, 0, 0, 0)
     _, rl = ref.varlen_attention(qkv.float(), 4, 4, 64, cu, 0.125, return_lse=True)
     _close(lse, rl, 1e-2, 1e-3)
 
