@@ -353,11 +353,13 @@ int launch_linear_t(const LinearParams& p, hipStream_t s) {
   if ((p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) && (!p.aux || p.ldaux <= 0)) return -3;
   if (p.M == 0) return 0;
   // 256 x 256 tiles (8 waves, 128 x 64 per wave: 25 % fewer LDS reads per MFMA, half the
-  // global->LDS traffic per FLOP) when the grid still covers the chip; 128 x 128 otherwise
+  // global->LDS traffic per FLOP) pay off on long reductions (K >= 2048: +30 % at 4096^3) when
+  // the grid still covers the chip; at K = 768 the 128 x 128 tile is faster
+  // (profiles/linear_gemm_vs_hipblaslt.md)
   int tile = p.tile;
   if (tile < 0) {
     const int64_t t256 = (int64_t)((p.M + 255) / 256) * (p.N / 256);
-    tile = (p.N % 256 == 0 && t256 >= 240) ? 1 : 0;
+    tile = (p.N % 256 == 0 && p.K >= 2048 && t256 >= 240) ? 1 : 0;
   }
   if (tile == 1 && p.N % 256 == 0) return launch_cfg<NN, 256, 256, 2, 4>(p, s);
   return launch_cfg<NN, 128, 128, 2, 2>(p, s);
