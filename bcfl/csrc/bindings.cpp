@@ -201,6 +201,42 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
 }
 
 // ------------------------------------------------------------------------------------------------
+// pooled-row attention (subset_attention.hip)
+std::vector<Tensor> subset_attn_fwd(Tensor qkv, Tensor cu, Tensor rows, int64_t max_s, int64_t nh,
+                                    int64_t nkv, int64_t d, double scale, bool causal, int64_t p8,
+                                    int64_t ka, int64_t kb) {
+  check_cuda(qkv, "qkv");
+  check_cuda(cu, "cu_seqlens");
+  check_cuda(rows, "rows");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "subset attention takes bf16");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && rows.scalar_type() == at::kInt, "cu / rows int32");
+  TORCH_CHECK(qkv.size(-1) == (nh + 2 * nkv) * d, "qkv width != (nh + 2 nkv) * d");
+  const int B = rows.numel();
+  TORCH_CHECK(cu.numel() >= B + 1, "cu_seqlens shorter than rows + 1");
+  auto out = torch::empty({B, nh * d}, qkv.options());
+  auto lse = torch::empty({B, nh}, qkv.options().dtype(torch::kFloat));
+  bcfl::SubsetAttnParams p{qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), cu.data_ptr<int>(),
+                           rows.data_ptr<int>(), B, (int)nh, (int)nkv, (int)d, (int)max_s,
+                           (float)scale, (int)causal, (uint32_t)p8, (uint32_t)ka, (uint32_t)kb};
+  check_rc(bcfl::launch_subset_attn_fwd(p, stream()), "subset_attn_fwd");
+  return {out, lse};
+}
+
+Tensor subset_attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, Tensor rows,
+                       int64_t max_s, int64_t nh, int64_t nkv, int64_t d, double scale,
+                       bool causal, int64_t p8, int64_t ka, int64_t kb) {
+  check_cuda(dout, "dout");
+  check_cuda(qkv, "qkv");
+  auto dqkv = torch::zeros_like(qkv);
+  bcfl::SubsetAttnBwdParams p{qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                              dqkv.data_ptr(), cu.data_ptr<int>(), rows.data_ptr<int>(),
+                              (int)rows.numel(), (int)nh, (int)nkv, (int)d, (int)max_s,
+                              (float)scale, (int)causal, (uint32_t)p8, (uint32_t)ka, (uint32_t)kb};
+  check_rc(bcfl::launch_subset_attn_bwd(p, stream()), "subset_attn_bwd");
+  return dqkv;
+}
+
+// ------------------------------------------------------------------------------------------------
 std::vector<Tensor> emb_ln_fwd(Tensor ids, Tensor pos, optional<Tensor> tt, Tensor word,
                                optional<Tensor> posw, optional<Tensor> typew, Tensor gamma,
                                Tensor beta, double eps, int64_t p8, int64_t ka, int64_t kb) {
@@ -573,6 +609,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("wgrad", &wgrad);
   m.def("linear_fwd", &linear_fwd);
+  m.def("subset_attn_fwd", &subset_attn_fwd);
+  m.def("subset_attn_bwd", &subset_attn_bwd);
   m.def("linear_dgrad", &linear_dgrad);
   m.def("wgrad_bias", &wgrad_bias);
   m.def("attn_fwd", &attn_fwd);

@@ -139,6 +139,34 @@ struct AttnBwdParams {
 // written by the forward, read by the backward kernels
 int attn_dropmask_words(int max_s);  // W
 int launch_attn_fwd(const AttnParams& p, hipStream_t s);
+
+// ---- subset_attention.hip: one pooled query row per sequence vs all its keys ------------------
+struct SubsetAttnParams {
+  const void* qkv;   // [T, (nh + 2 nkv) * d] bf16
+  void* out;         // [B, nh * d] bf16
+  float* lse;        // [B, nh]
+  const int* cu;     // [B + 1]
+  const int* rows;   // [B] absolute token index of each sequence's pooled row
+  int B, nh, nkv, d, max_s;
+  float scale;
+  int causal;
+  uint32_t p8, ka, kb;
+};
+struct SubsetAttnBwdParams {
+  const void* qkv;
+  const void* out;
+  const void* dout;  // [B, nh * d]
+  const float* lse;
+  void* dqkv;        // [T, (nh + 2 nkv) * d], zero-filled by the caller
+  const int* cu;
+  const int* rows;
+  int B, nh, nkv, d, max_s;
+  float scale;
+  int causal;
+  uint32_t p8, ka, kb;
+};
+int launch_subset_attn_fwd(const SubsetAttnParams& p, hipStream_t s);
+int launch_subset_attn_bwd(const SubsetAttnBwdParams& p, hipStream_t s);
 int launch_attn_bwd(const AttnBwdParams& p, hipStream_t s);
 
 }  // namespace bcfl

@@ -390,6 +390,30 @@ def varlen_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, cu_host: Seque
                                 p8, ka, kb)
 
 
+class _SubsetAttn(torch.autograd.Function):
+    """Pooled-row attention on the GPU (subset_attention.hip, forward + backward)."""
+
+    @staticmethod
+    def forward(ctx, qkv, rows, cu, max_s, nh, nkv, d, scale, causal, p8, ka, kb):
+        out, lse = native().subset_attn_fwd(qkv, cu, rows, int(max_s), int(nh), int(nkv), int(d),
+                                            float(scale), bool(causal), int(p8), int(ka), int(kb))
+        ctx.save_for_backward(qkv, rows, cu, out, lse)
+        ctx.cfg = (max_s, nh, nkv, d, scale, causal, p8, ka, kb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, rows, cu, out, lse = ctx.saved_tensors
+        max_s, nh, nkv, d, scale, causal, p8, ka, kb = ctx.cfg
+        dqkv = native().subset_attn_bwd(dout.contiguous(), qkv, out, lse, cu, rows, int(max_s),
+                                        int(nh), int(nkv), int(d), float(scale), bool(causal),
+                                        int(p8), int(ka), int(kb))
+        return (dqkv,) + (None,) * 11
+
+
+SUBSET_ATTN_MAX_KEYS = 6144  # subset_attention.hip LDS rows
+
+
 def query_subset_attention(qkv: torch.Tensor, rows: torch.Tensor, cu_seqlens: torch.Tensor,
                            max_seqlen: int, num_heads: int, num_kv_heads: int, head_dim: int,
                            dropout_p: float = 0.0, training: bool = False, causal: bool = False,
@@ -407,6 +431,11 @@ def query_subset_attention(qkv: torch.Tensor, rows: torch.Tensor, cu_seqlens: to
     scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
     p8, ka, kb = _keys(dropout_p, training)
     B = int(rows.shape[0])
+    if (use_native(qkv, "subset_attn") and qkv.dtype == torch.bfloat16 and head_dim in (32, 64, 128)
+            and int(max_seqlen) <= SUBSET_ATTN_MAX_KEYS):
+        return _SubsetAttn.apply(qkv.contiguous(), rows.to(torch.int32).contiguous(),
+                                 cu_seqlens.to(torch.int32).contiguous(), int(max_seqlen),
+                                 num_heads, num_kv_heads, head_dim, scale, causal, p8, ka, kb)
     dev = qkv.device
     nh, nkv, d = num_heads, num_kv_heads, head_dim
     cu = cu_seqlens[:B + 1].long()

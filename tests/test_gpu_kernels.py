@@ -457,3 +457,33 @@ def test_fused_ffn_autograd_matches_reference():
         # (fused epilogue vs bf16 GEMM output + separate bias/GELU): compare normwise
         err = ((a.float() - b.float()).norm() / b.float().norm()).item()
         assert err < 1e-2, (name, err)
+
+
+@pytest.mark.parametrize("nh,nkv,d,causal,p", [(12, 12, 64, False, 0.0), (12, 12, 64, False, 0.1),
+                                               (8, 2, 128, True, 0.0), (4, 4, 32, False, 0.1)])
+def test_subset_attention_matches_torch_reference(nh, nkv, d, causal, p):
+    """subset_attention.hip (fwd + bwd, dropout keep bits, GQA, causal last-token rows) == the
+    torch implementation of the same pooled-row attention (BCFL_TORCH_OPS=subset_attn)."""
+    import os
+    torch.manual_seed(3)
+    lens = np.array([37, 300, 5, 129, 64])
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    T = int(cu[-1])
+    rows = torch.from_numpy(cu[1:] - 1 if causal else cu[:-1]).to(DEV)
+    cu_d = torch.from_numpy(cu).to(DEV)
+    x0 = torch.randn(T, (nh + 2 * nkv) * d, device=DEV).bfloat16()
+    g = torch.randn(len(lens), nh * d, device=DEV).bfloat16()
+    ops.rng.global_rng().load_state({"seed": 5, "counter": 0})
+    res = {}
+    for route in ("bcfl", "torch"):
+        os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "subset_attn"
+        try:
+            ops.rng.global_rng().load_state({"seed": 5, "counter": 0})
+            x = x0.clone().requires_grad_(True)
+            o = ops.query_subset_attention(x, rows, cu_d, int(lens.max()), nh, nkv, d, p, True, causal)
+            o.backward(g)
+            res[route] = (o.float(), x.grad.float())
+        finally:
+            os.environ["BCFL_TORCH_OPS"] = ""
+    _close(res["bcfl"][0], res["torch"][0], 2e-2, 2e-2)
+    _close(res["bcfl"][1], res["torch"][1], 2e-2, 2e-2)
