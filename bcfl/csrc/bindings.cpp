@@ -200,6 +200,16 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
   return dqkv;
 }
 
+// dropout multiplier tensor (keep / (1 - p) or 0), shape [n], like `like`'s dtype / device
+Tensor drop_mask(Tensor like, int64_t n, int64_t p8, int64_t ka, int64_t kb) {
+  TORCH_CHECK(like.is_cuda(), "drop_mask: GPU tensor required");
+  auto m = torch::empty({n}, like.options());
+  check_rc(bcfl::launch_drop_mask(m.data_ptr(), dt_of(like), n, (uint32_t)p8, (uint32_t)ka,
+                                  (uint32_t)kb, stream()),
+           "drop_mask");
+  return m;
+}
+
 // ------------------------------------------------------------------------------------------------
 // pooled-row attention (subset_attention.hip)
 std::vector<Tensor> subset_attn_fwd(Tensor qkv, Tensor cu, Tensor rows, int64_t max_s, int64_t nh,
@@ -609,6 +619,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("wgrad", &wgrad);
   m.def("linear_fwd", &linear_fwd);
+  m.def("drop_mask", &drop_mask);
   m.def("subset_attn_fwd", &subset_attn_fwd);
   m.def("subset_attn_bwd", &subset_attn_bwd);
   m.def("linear_dgrad", &linear_dgrad);

@@ -376,7 +376,37 @@ __global__ __launch_bounds__(EW_THREADS) void block_sketch_kernel(const TX* __re
   }
 }
 
+// dropout multiplier m[i] = keep(i) / (1 - p) or 0 (bcfl/ops/rng.py element layout): the pooled
+// [B, H] head dropout applies it with one multiply forward and one backward
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void drop_mask_kernel(T* __restrict__ m, int64_t n,
+                                                               uint32_t p8, uint32_t ka,
+                                                               uint32_t kb, float scale) {
+  for (int64_t i4 = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i4 * 4 < n;
+       i4 += (int64_t)gridDim.x * EW_THREADS) {
+    const uint32_t h = hash32((uint32_t)i4, ka, kb);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t i = i4 * 4 + e;
+      if (i < n) m[i] = (T)(((h >> (8 * e)) & 0xffu) >= p8 ? scale : 0.f);
+    }
+  }
+}
+
 }  // namespace
+
+int launch_drop_mask(void* m, int dt, int64_t n, uint32_t p8, uint32_t ka, uint32_t kb,
+                     hipStream_t s) {
+  if (n <= 0) return 0;
+  const float scale = 256.0f / (256.0f - (float)p8);  // host copy of keep_scale()
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(drop_mask_kernel<__bf16>, dim3(ew_grid((n + 3) / 4)), dim3(EW_THREADS), 0, s,
+                       (__bf16*)m, n, p8, ka, kb, scale);
+  else
+    hipLaunchKernelGGL(drop_mask_kernel<float>, dim3(ew_grid((n + 3) / 4)), dim3(EW_THREADS), 0, s,
+                       (float*)m, n, p8, ka, kb, scale);
+  return 0;
+}
 
 int launch_bias_act_fwd(const void* y, const void* bias, void* out, int64_t rows, int N, int act,
                         int dt, hipStream_t s) {

@@ -147,9 +147,19 @@ class Federation:
             for c in self.local_clients:
                 self.client_master[c] = self.flat.master.detach().clone()
         self.lanes = self._build_lanes(vocab, mdtype)
+        # lanes train every hosted client IN PLACE on its own resident buffers (FlatParams.rebind):
+        # no per-client master copies in / out of a lane replica
+        self.client_param: Dict[int, torch.Tensor] = {}
+        if self.lanes:
+            for c in self.local_clients:
+                self.client_param[c] = torch.empty(self.flat.numel, dtype=self.flat.dtype,
+                                                   device=self.device)
+                ops.cast_copy_(self.client_param[c], self.client_master[c])
         self.drift = DriftCorrection(cfg.drift_correction, cfg.drift_correction_scale,
                                      self.local_clients, self.flat.numel, self.device)
         ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else len(self.lanes) <= 1
+        if cfg.deterministic:
+            ov = False  # the overlapped path's gradients are not bitwise reproducible
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
         self.global_master: Optional[torch.Tensor] = None
         if cfg.mode == "server":
@@ -278,7 +288,7 @@ class Federation:
         cfg = self.cfg
         for c in lane.clients:
             with self._on(lane):
-                lane.flat.load_master(self.client_master[c])
+                lane.flat.rebind(self.client_master[c], self.client_param[c])
                 if cfg.keep_optimizer_state and c in self.client_opt:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
@@ -320,7 +330,6 @@ class Federation:
                     out["local_eval"][c] = lane.trainer.evaluate_device(self.test_batches(c, r))
                 out["roots"][c] = (ops.merkle_root_deferred(lane.flat.master)
                                    if self.ledger is not None and not self._gossip_roots else None)
-                self.client_master[c].copy_(lane.flat.master)
                 if cfg.keep_optimizer_state:
                     self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
                                           for k, v in lane.opt.state_dict().items()}
@@ -721,14 +730,20 @@ class Federation:
         use_v = self.prev_verdicts if cfg.async_gossip else v
         W = mixing_matrix(self.nbrs, cfg.mixing, use_v.rejected)
         with self.timer.phase("comm"):
-            info = self.gossip.end_of_round(r, W, None if self.multi else {self.local_clients[0]: self.flat.param},
+            pout = (self.client_param if self.lanes else
+                    None if self.multi else {self.local_clients[0]: self.flat.param})
+            info = self.gossip.end_of_round(r, W, pout,
                                             steps={c: losses[c]["batches"] for c in losses})
         recs += self._gossip_records(r, recs)
         self.prev_verdicts = v
         for c in self.local_clients:
             self.drift.after_mix(c, self.client_master[c] if self.multi else self.flat.master)
         if self.multi:  # evaluate this rank's first client's mixed model
-            self.flat.load_master(self.client_master[self.local_clients[0]])
+            c0 = self.local_clients[0]
+            if self.lanes:
+                self.flat.rebind(self.client_master[c0], self.client_param[c0])
+            else:
+                self.flat.load_master(self.client_master[c0])
         ge = self._eval_global(r) if cfg.eval_global else None
         loc = []
         for c, t in local_eval.items():
@@ -953,6 +968,8 @@ class Federation:
             self.global_master.copy_(self.flat.master)
         for c in self.client_master:
             self.client_master[c].copy_(self.flat.master)
+            if c in self.client_param:
+                ops.cast_copy_(self.client_param[c], self.client_master[c])
         if self.gossip is not None:
             self.gossip.seed_replicas(self.flat.master)
         self.start_round = int(st["round"]) + 1
@@ -982,6 +999,8 @@ class Federation:
             self.client_rng[int(c)] = dict(v)
         for c, t in st["client_master"].items():
             self.client_master[int(c)].copy_(t)
+            if int(c) in self.client_param:
+                ops.cast_copy_(self.client_param[int(c)], self.client_master[int(c)])
         self.flat.load_master(st["master"].to(self.device))
         for c, o in st["client_opt"].items():
             self.client_opt[int(c)] = {"m": o["m"].to(self.device), "v": o["v"].to(self.device),

@@ -580,5 +580,8 @@ def dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     p8, ka, kb = _keys(p, training)
     if p8 == 0:
         return x
+    if use_native(x, "dropout") and x.dtype in (torch.bfloat16, torch.float32):
+        # one hash kernel -> multiplier m = keep / (1 - p); autograd: one multiply each way
+        return x * native().drop_mask(x, x.numel(), int(p8), int(ka), int(kb)).view_as(x)
     keep = _rng.keep_mask(x.numel(), p8, ka, kb, device=x.device).view_as(x)
     return x * keep.to(x.dtype) * _rng.keep_scale(p8)

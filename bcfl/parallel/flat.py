@@ -93,6 +93,15 @@ class FlatParams:
         if self.master is not self.param:
             ops.cast_copy_(self.param, self.master)
 
+    def rebind(self, master: torch.Tensor, param: torch.Tensor):
+        """Point this replica at ANOTHER client's buffers (fp32 master + compute-dtype param of
+        the same layout): the model's parameter views move, nothing is copied. Client lanes use
+        this to train each hosted client in place on its own resident state."""
+        if master.numel() != self.numel or param.numel() != self.numel or param.dtype != self.dtype:
+            raise ValueError("rebind: buffers must match this FlatParams' layout and dtype")
+        self.master, self.param = master, param
+        self._bind()
+
     @torch.no_grad()
     def load_master(self, src: torch.Tensor):
         self.master.copy_(src)
