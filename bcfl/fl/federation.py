@@ -241,7 +241,9 @@ class Federation:
         cfg = self.cfg
         if not (cfg.mode == "serverless" and self.multi and not cfg.compat_chain):
             return []
-        if cfg.client_lanes:
+        if cfg.deterministic:
+            n = 1  # concurrent lanes reorder library reductions (timing-dependent, ~1e-7)
+        elif cfg.client_lanes:
             n = cfg.client_lanes
         elif not self.is_cuda:
             n = 1
