@@ -67,6 +67,12 @@ class LoRA(nn.Module):
         d = outs[0] if len(outs) == 1 else torch.cat(outs, dim=1)
         return d * self.scale
 
+    def fused(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        """x W^T + this adapter's delta, WITHOUT materialising the delta as a separate pass:
+        the low-rank product writes the output buffer and the base GEMM accumulates into it
+        (ops.lora_linear; GPU). CPU / unsupported: the unfused reference."""
+        return ops.lora_linear(x, w, self.A, list(self.B), self.scale)
+
 
 class LlamaLayer(nn.Module):
     def __init__(self, cfg: LlamaConfig, device, dtype, lora: bool):
@@ -93,9 +99,7 @@ class LlamaLayer(nn.Module):
         c = self.cfg
         nh, nkv, d = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         h = ops.rmsnorm(x, self.in_ln, c.rms_norm_eps)
-        qkv = ops.linear(h, self.qkv_weight)
-        if self.lora:
-            qkv = qkv + self.lora_qkv(h)
+        qkv = self.lora_qkv.fused(h, self.qkv_weight) if self.lora else ops.linear(h, self.qkv_weight)
         qkv = ops.rope(qkv, batch.position_ids, cos, sin, nh, nkv, d)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
@@ -104,18 +108,13 @@ class LlamaLayer(nn.Module):
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen, nh,
                                              nkv, d, 0.0, self.training, causal=True)
             x = x.index_select(0, rows.long())
-        o = ops.linear(ctx, self.o_weight)
-        if self.lora:
-            o = o + self.lora_o(ctx)
+        o = self.lora_o.fused(ctx, self.o_weight) if self.lora else ops.linear(ctx, self.o_weight)
         x = x + o
         h2 = ops.rmsnorm(x, self.post_ln, c.rms_norm_eps)
-        gu = ops.linear(h2, self.gate_up_weight)
-        if self.lora:
-            gu = gu + self.lora_gate_up(h2)
+        gu = (self.lora_gate_up.fused(h2, self.gate_up_weight) if self.lora
+              else ops.linear(h2, self.gate_up_weight))
         a = ops.swiglu(gu)
-        dn = ops.linear(a, self.down_weight)
-        if self.lora:
-            dn = dn + self.lora_down(a)
+        dn = self.lora_down.fused(a, self.down_weight) if self.lora else ops.linear(a, self.down_weight)
         return x + dn
 
 

@@ -24,7 +24,7 @@ from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
-           "linear_act", "linear_after_act", "gemm_supported",
+           "linear_act", "linear_after_act", "gemm_supported", "lora_linear",
            "query_subset_attention", "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
@@ -245,6 +245,60 @@ class _LinearAfterAct(torch.autograd.Function):
             dpre = native().linear_dgrad(g2, w, pre.reshape(-1, K), ctx.act_id).view(pre.shape)
         dw, _ = _weight_grads(ctx, g2, h2, w, None, ctx.needs_input_grad[2], False)
         return None, dpre, dw, None
+
+
+class _LoRALinear(torch.autograd.Function):
+    """y = x W^T + s (x A^T) Bbd^T for a FROZEN base W and LoRA adapters (A stacked [n r, K], one
+    B_i [o_i, r] per output block i; Bbd = block-diagonal [N, n r]).
+
+    Forward: ONE low-rank GEMM writes (s xa) Bbd^T into the output buffer, then the base GEMM
+    accumulates into it in place (beta = 1) — no cat / scale / add passes over [T, N].
+    Backward: dx = g W + s (g Bbd) A with the second product accumulated in place into the first;
+    dA = s (g Bbd)^T x; dB_i = s g_i^T xa_i (block-diagonal of one [N, n r] GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, w, a, s, sizes, *bs):
+        x2 = x.reshape(-1, x.shape[-1])
+        xa = x2 @ a.t()                                   # [M, n r]
+        bbd = torch.block_diag(*bs)                       # [N, n r]
+        y = torch.mm(xa * s, bbd.t())                     # scale on the [M, n r] side
+        y.addmm_(x2, w.t())                               # base GEMM accumulates in place
+        ctx.save_for_backward(x2, w, a, xa, bbd)
+        ctx.s, ctx.sizes, ctx.xshape = s, sizes, x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w, a, xa, bbd = ctx.saved_tensors
+        s, sizes = ctx.s, ctx.sizes
+        g2 = g.reshape(-1, w.shape[0])
+        gb = g2 @ bbd                                     # [M, n r]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = g2 @ w
+            dx.addmm_(gb, a, alpha=s)                     # LoRA input gradient, in place
+            dx = dx.view(ctx.xshape)
+        da = (gb.t() @ x2).mul_(s) if ctx.needs_input_grad[2] else None
+        dbs = [None] * len(sizes)
+        if any(ctx.needs_input_grad[5:]):
+            full = (g2.t() @ xa).mul_(s)                  # [N, n r]; block i = dB_i
+            r = xa.shape[1] // len(sizes)
+            o = 0
+            for i, n in enumerate(sizes):
+                dbs[i] = full[o:o + n, i * r:(i + 1) * r].contiguous()
+                o += n
+        return (dx, None, da, None, None, *dbs)
+
+
+def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, bs, s: float) -> torch.Tensor:
+    """Frozen base projection + LoRA delta, fused on the GPU (see :class:`_LoRALinear`)."""
+    if use_native(x, "lora") and not w.requires_grad and x.dtype == torch.bfloat16:
+        return _LoRALinear.apply(x, w, a, float(s), tuple(int(b.shape[0]) for b in bs), *bs)
+    xa = linear(x, a)
+    r = a.shape[0] // len(bs)
+    outs = [linear(xa[..., i * r:(i + 1) * r], b) for i, b in enumerate(bs)]
+    d = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
+    return linear(x, w) + d * s
 
 
 def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:

@@ -507,3 +507,32 @@ def test_native_dropout_mask_matches_hash_layout():
         os.environ["BCFL_TORCH_OPS"] = ""
     assert torch.equal(y == 0, r == 0)           # identical keep decisions
     _close(y, r, 1e-2, 1e-2)
+
+
+def test_lora_linear_fused_matches_unfused():
+    """ops.lora_linear (low-rank product written first, frozen base GEMM accumulating in place;
+    custom backward) == the unfused x W^T + cat(xa_i B_i^T) * s path, forward and gradients."""
+    import os
+    torch.manual_seed(4)
+    T, K, r = 1000, 512, 16
+    sizes = [512, 128, 128]
+    x0 = torch.randn(T, K, device=DEV).bfloat16()
+    w = (torch.randn(sum(sizes), K, device=DEV) * 0.05).bfloat16()
+    a0 = (torch.randn(len(sizes) * r, K, device=DEV) * 0.05).bfloat16()
+    b0 = [(torch.randn(n, r, device=DEV) * 0.05).bfloat16() for n in sizes]
+    g = torch.randn(T, sum(sizes), device=DEV).bfloat16()
+    res = {}
+    for route in ("bcfl", "torch"):
+        os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "lora"
+        try:
+            x = x0.clone().requires_grad_(True)
+            a = a0.clone().requires_grad_(True)
+            bs = [b.clone().requires_grad_(True) for b in b0]
+            y = ops.lora_linear(x, w, a, bs, 2.0)
+            y.backward(g)
+            res[route] = [y, x.grad, a.grad] + [b.grad for b in bs]
+        finally:
+            os.environ["BCFL_TORCH_OPS"] = ""
+    for u, v in zip(res["bcfl"], res["torch"]):
+        err = ((u.float() - v.float()).norm() / v.float().norm()).item()
+        assert err < 1e-2, err
