@@ -200,6 +200,31 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
   return dqkv;
 }
 
+// cross-entropy (xent.hip): {mean loss (fp32 scalar), dloss/dlogits}; eval statistics in place
+std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
+  check_cuda(logits, "logits");
+  check_cuda(labels, "labels");
+  TORCH_CHECK(logits.dim() == 2 && labels.scalar_type() == at::kInt && labels.numel() == logits.size(0),
+              "xent: logits [B, C], labels [B] int32");
+  auto loss = torch::empty({}, logits.options().dtype(torch::kFloat));
+  auto grad = torch::empty_like(logits);
+  check_rc(bcfl::launch_xent_fwd(logits.data_ptr(), labels.data_ptr<int>(), logits.size(0),
+                                 logits.size(1), loss.data_ptr<float>(), grad.data_ptr(),
+                                 dt_of(logits), stream()),
+           "xent_fwd");
+  return {loss, grad};
+}
+
+void xent_stats(Tensor logits, Tensor labels, Tensor acc4) {
+  check_cuda(logits, "logits");
+  check_cuda(labels, "labels");
+  TORCH_CHECK(acc4.is_cuda() && acc4.scalar_type() == at::kDouble && acc4.numel() >= 4, "acc4: fp64[4]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() == logits.size(0), "labels [B] int32");
+  check_rc(bcfl::launch_xent_stats(logits.data_ptr(), labels.data_ptr<int>(), logits.size(0),
+                                   logits.size(1), acc4.data_ptr<double>(), dt_of(logits), stream()),
+           "xent_stats");
+}
+
 // dropout multiplier tensor (keep / (1 - p) or 0), shape [n], like `like`'s dtype / device
 Tensor drop_mask(Tensor like, int64_t n, int64_t p8, int64_t ka, int64_t kb) {
   TORCH_CHECK(like.is_cuda(), "drop_mask: GPU tensor required");
@@ -619,6 +644,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("wgrad", &wgrad);
   m.def("linear_fwd", &linear_fwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_stats", &xent_stats);
   m.def("drop_mask", &drop_mask);
   m.def("subset_attn_fwd", &subset_attn_fwd);
   m.def("subset_attn_bwd", &subset_attn_bwd);

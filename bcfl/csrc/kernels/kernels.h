@@ -41,6 +41,11 @@ int launch_rmsnorm_bwd(const void* dout, const void* x, const void* w, const flo
                        float* partial, int nblk, int T, int H, int dt, hipStream_t s);
 
 // ---- elementwise.hip -----------------------------------------------------------------------------
+// ---- xent.hip: classifier cross-entropy ------------------------------------------------------
+int launch_xent_fwd(const void* logits, const int* labels, int B, int C, float* loss, void* grad,
+                    int dt, hipStream_t s);
+int launch_xent_stats(const void* logits, const int* labels, int B, int C, double* acc4, int dt,
+                      hipStream_t s);
 int launch_drop_mask(void* m, int dt, int64_t n, uint32_t p8, uint32_t ka, uint32_t kb,
                      hipStream_t s);
 int launch_bias_act_fwd(const void* y, const void* bias, void* out, int64_t rows, int N, int act,

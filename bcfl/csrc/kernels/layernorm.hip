@@ -118,32 +118,36 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
   }
   const int stride = gridDim.x * LN_WAVES;
   int row = blockIdx.x * LN_WAVES + wid;
-  float nd[NCH][4], nz[NCH][4], nmean = 0.f, nrstd = 0.f;
-  auto fetch = [&](int r) {
+  // TWO rows in flight per wave (register sets A and B, alternating): the loads of row r+2s are
+  // issued before row r's math, so each wave keeps ~2 x 48 B per lane outstanding
+  struct RowBuf {
+    float d[NCH][4], z[NCH][4];
+    float mean = 0.f, rstd = 0.f;
+  };
+  RowBuf ba, bb;
+  auto fetch = [&](RowBuf& rb, int r) {
     if (r < T) {
       const size_t bs = (size_t)r * H;
-      nmean = mean_in[r];
-      nrstd = rstd_in[r];
+      rb.mean = mean_in[r];
+      rb.rstd = rstd_in[r];
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int col = (lane + i * WAVE) * 4;
         if (col < H) {
-          Vec4<TA>::load(dout + bs + col, nd[i]);
-          Vec4<TA>::load(z + bs + col, nz[i]);
+          Vec4<TA>::load(dout + bs + col, rb.d[i]);
+          Vec4<TA>::load(z + bs + col, rb.z[i]);
         }
       }
     }
   };
-  fetch(row);
-  for (; row < T; row += stride) {
-    const size_t base = (size_t)row * H;
-    const float mean = nmean, rstd = nrstd;
+  auto process = [&](const RowBuf& rb, int r) {
+    const size_t base = (size_t)r * H;
+    const float mean = rb.mean, rstd = rb.rstd;
     float d[NCH][4], xh[NCH][4], g[NCH][4];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { d[i][k] = nd[i][k]; xh[i][k] = nz[i][k]; }
-    fetch(row + stride);  // in flight during this row's math
+      for (int k = 0; k < 4; ++k) { d[i][k] = rb.d[i][k]; xh[i][k] = rb.z[i][k]; }
     uint32_t hs[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
@@ -182,6 +186,17 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
         if (dy_out) Vec4<TA>::store(dy_out + base + col, dy);
       }
     }
+  };
+  fetch(ba, row);
+  fetch(bb, row + stride);
+  for (; row < T; row += 2 * stride) {
+    RowBuf cur = ba;
+    fetch(ba, row + 2 * stride);  // in flight during this row's and the next row's math
+    process(cur, row);
+    if (row + stride >= T) break;
+    cur = bb;
+    fetch(bb, row + 3 * stride);
+    process(cur, row + stride);
   }
   // combine the block's waves
 #pragma unroll
@@ -915,7 +930,7 @@ inline bool use8(int H) { return H % 8 == 0 && H <= 2048; }
 // ~3 rows per row-stream: enough waves to hide latency at BERT batch sizes while the partial
 // row-set stays small for colsum. (Same count for the wave-per-row and half-wave-per-row kernels.)
 int bwd_blocks(int T) {
-  int b = (T + 8 * 3 - 1) / (8 * 3);
+  int b = (T + 4 * 4 - 1) / (4 * 4);  // ~4 rows per wave
   return b < 1 ? 1 : (b > 1024 ? 1024 : b);
 }
 

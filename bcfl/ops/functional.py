@@ -24,7 +24,7 @@ from ._native import native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
-           "linear_act", "linear_after_act", "gemm_supported", "lora_linear",
+           "linear_act", "linear_after_act", "gemm_supported", "lora_linear", "xent_stats_",
            "query_subset_attention", "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
@@ -624,8 +624,40 @@ def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
     return ref.swiglu(gate_up)
 
 
+class _XEnt(torch.autograd.Function):
+    """K9: mean softmax cross-entropy, loss and gradient from ONE kernel (xent.hip)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        loss, grad = native().xent_fwd(logits, labels)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None
+
+
 def cross_entropy(logits, labels):
+    if use_native(logits, "xent") and logits.dim() == 2 and logits.dtype in (torch.bfloat16,
+                                                                            torch.float32):
+        return _XEnt.apply(logits.contiguous(), labels.to(torch.int32).contiguous())
     return torch.nn.functional.cross_entropy(logits.float(), labels.long())
+
+
+@torch.no_grad()
+def xent_stats_(logits: torch.Tensor, labels: torch.Tensor, acc4: torch.Tensor) -> None:
+    """acc4 (fp64 [4]) += [correct, count, sum CE, sum CE / count] of one evaluation batch."""
+    if use_native(logits, "xent") and logits.dtype in (torch.bfloat16, torch.float32):
+        native().xent_stats(logits.contiguous(), labels.to(torch.int32).contiguous(), acc4)
+        return
+    lg, lab = logits.float(), labels.long()
+    ce = torch.nn.functional.cross_entropy(lg, lab, reduction="sum")
+    acc4[0] += (lg.argmax(-1) == lab).sum()
+    acc4[1] += lab.numel()
+    acc4[2] += ce
+    acc4[3] += ce / lab.numel()
 
 
 def dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:

@@ -536,3 +536,24 @@ def test_lora_linear_fused_matches_unfused():
     for u, v in zip(res["bcfl"], res["torch"]):
         err = ((u.float() - v.float()).norm() / v.float().norm()).item()
         assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("B,C", [(32, 2), (7, 41), (256, 40), (300, 3)])
+def test_xent_kernels_match_torch(B, C):
+    torch.manual_seed(B + C)
+    lg = (torch.randn(B, C, device=DEV) * 3).bfloat16().requires_grad_(True)
+    lab = torch.randint(0, C, (B,), device=DEV)
+    loss = ops.cross_entropy(lg, lab)
+    (loss * 2.0).backward()
+    ref_lg = lg.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(ref_lg, lab)
+    (ref * 2.0).backward()
+    _close(loss, ref, 1e-4, 1e-4)
+    _close(lg.grad, ref_lg.grad, 1e-3, 2e-2)
+    acc = torch.zeros(4, dtype=torch.float64, device=DEV)
+    ops.xent_stats_(lg.detach(), lab, acc)
+    ops.xent_stats_(lg.detach(), lab, acc)
+    ce = torch.nn.functional.cross_entropy(lg.detach().float(), lab, reduction="sum").double()
+    want = torch.stack([2 * (lg.detach().float().argmax(-1) == lab).sum().double(),
+                        torch.tensor(2.0 * B, device=DEV, dtype=torch.float64), 2 * ce, 2 * ce / B])
+    torch.testing.assert_close(acc, want, rtol=1e-4, atol=1e-3)
