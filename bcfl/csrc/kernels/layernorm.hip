@@ -118,36 +118,32 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
   }
   const int stride = gridDim.x * LN_WAVES;
   int row = blockIdx.x * LN_WAVES + wid;
-  // TWO rows in flight per wave (register sets A and B, alternating): the loads of row r+2s are
-  // issued before row r's math, so each wave keeps ~2 x 48 B per lane outstanding
-  struct RowBuf {
-    float d[NCH][4], z[NCH][4];
-    float mean = 0.f, rstd = 0.f;
-  };
-  RowBuf ba, bb;
-  auto fetch = [&](RowBuf& rb, int r) {
+  float nd[NCH][4], nz[NCH][4], nmean = 0.f, nrstd = 0.f;
+  auto fetch = [&](int r) {
     if (r < T) {
       const size_t bs = (size_t)r * H;
-      rb.mean = mean_in[r];
-      rb.rstd = rstd_in[r];
+      nmean = mean_in[r];
+      nrstd = rstd_in[r];
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int col = (lane + i * WAVE) * 4;
         if (col < H) {
-          Vec4<TA>::load(dout + bs + col, rb.d[i]);
-          Vec4<TA>::load(z + bs + col, rb.z[i]);
+          Vec4<TA>::load(dout + bs + col, nd[i]);
+          Vec4<TA>::load(z + bs + col, nz[i]);
         }
       }
     }
   };
-  auto process = [&](const RowBuf& rb, int r) {
-    const size_t base = (size_t)r * H;
-    const float mean = rb.mean, rstd = rb.rstd;
+  fetch(row);
+  for (; row < T; row += stride) {
+    const size_t base = (size_t)row * H;
+    const float mean = nmean, rstd = nrstd;
     float d[NCH][4], xh[NCH][4], g[NCH][4];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { d[i][k] = rb.d[i][k]; xh[i][k] = rb.z[i][k]; }
+      for (int k = 0; k < 4; ++k) { d[i][k] = nd[i][k]; xh[i][k] = nz[i][k]; }
+    fetch(row + stride);  // in flight during this row's math
     uint32_t hs[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
@@ -186,17 +182,6 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
         if (dy_out) Vec4<TA>::store(dy_out + base + col, dy);
       }
     }
-  };
-  fetch(ba, row);
-  fetch(bb, row + stride);
-  for (; row < T; row += 2 * stride) {
-    RowBuf cur = ba;
-    fetch(ba, row + 2 * stride);  // in flight during this row's and the next row's math
-    process(cur, row);
-    if (row + stride >= T) break;
-    cur = bb;
-    fetch(bb, row + 3 * stride);
-    process(cur, row + stride);
   }
   // combine the block's waves
 #pragma unroll
@@ -930,7 +915,7 @@ inline bool use8(int H) { return H % 8 == 0 && H <= 2048; }
 // ~3 rows per row-stream: enough waves to hide latency at BERT batch sizes while the partial
 // row-set stays small for colsum. (Same count for the wave-per-row and half-wave-per-row kernels.)
 int bwd_blocks(int T) {
-  int b = (T + 4 * 4 - 1) / (4 * 4);  // ~4 rows per wave
+  int b = (T + 8 * 3 - 1) / (8 * 3);
   return b < 1 ? 1 : (b > 1024 ? 1024 : b);
 }
 

@@ -55,12 +55,27 @@ __device__ __forceinline__ float dot_row(const float (&q)[(HD + 63) / 64], const
   return wave_sum(a);
 }
 
+// thread-per-key dot product: q (fp32, LDS broadcast) . row[0:HD] (bf16, 16-byte loads)
+template <int HD>
+__device__ __forceinline__ float dot_q_row(const float* __restrict__ qs, const bf16_t* row) {
+  float a = 0.f;
+#pragma unroll
+  for (int c = 0; c < HD; c += 8) {
+    float v[8];
+    Vec8<bf16_t>::load(row + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a += qs[c + e] * v[e];
+  }
+  return a;
+}
+
 template <int HD>
 __global__ __launch_bounds__(SA_THREADS) void subset_attn_fwd_kernel(SubsetAttnParams p) {
   constexpr int NC = (HD + 63) / 64;
   __shared__ float sc[SA_MAXK];
   __shared__ float red[SA_WAVES];
   __shared__ float opart[SA_WAVES][HD];
+  __shared__ float qs[HD];
   const int b = blockIdx.x, hk = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int start = p.cu[b];
@@ -75,19 +90,16 @@ __global__ __launch_bounds__(SA_THREADS) void subset_attn_fwd_kernel(SubsetAttnP
   const float sdrop = p.p8 ? keep_scale(p.p8) : 1.f;
   for (int g = 0; g < grp; ++g) {
     const int h = hk * grp + g;
-    float q[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int d = lane + 64 * c;
-      q[c] = d < HD ? bf2f(qkv[(size_t)qrow * rs + h * HD + d]) * p.scale : 0.f;
-    }
+    for (int d = threadIdx.x; d < HD; d += SA_THREADS)
+      qs[d] = bf2f(qkv[(size_t)qrow * rs + h * HD + d]) * p.scale;
+    __syncthreads();
     float mx = -INFINITY;
-    for (int j = w; j < L; j += SA_WAVES) {
-      const float s = dot_row<HD>(q, kbase + (size_t)j * rs, lane);
-      if (lane == 0) sc[j] = s;
+    for (int j = threadIdx.x; j < L; j += SA_THREADS) {  // one key per thread
+      const float s = dot_q_row<HD>(qs, kbase + (size_t)j * rs);
+      sc[j] = s;
       mx = fmaxf(mx, s);
     }
-    mx = block_reduce(mx, red, true);  // (its barriers also publish sc)
+    mx = block_reduce(mx, red, true);
     float sum = 0.f;
     for (int j = threadIdx.x; j < L; j += SA_THREADS) {
       const float e = __expf(sc[j] - mx);
@@ -145,6 +157,7 @@ __global__ __launch_bounds__(SA_THREADS) void subset_attn_bwd_kernel(SubsetAttnB
   __shared__ float dpr[SA_MAXK];  // dP_j = keep_j c (dO . v_j)
   __shared__ float red[SA_WAVES];
   __shared__ float qpart[SA_WAVES][HD];
+  __shared__ float qs[HD], dos[HD];
   const int b = blockIdx.x, hk = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int start = p.cu[b];
@@ -172,21 +185,21 @@ __global__ __launch_bounds__(SA_THREADS) void subset_attn_bwd_kernel(SubsetAttnB
     const float delta = wave_sum(delta_part);  // dO . O = sum_j P_j dP_j (every wave has it)
     const float lse = p.lse[(size_t)b * p.nh + h];
     const uint32_t erow = (uint32_t)(qrow * p.nh + h) * (uint32_t)SA_DROP_STRIDE;
-    for (int j = w; j < L; j += SA_WAVES) {
-      const bf16_t* row = qkv + (size_t)(start + j) * rs;
-      const float s = dot_row<HD>(q, row + koff, lane);
-      float dpv = 0.f;
+    if (w == 0) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int d = lane + 64 * c;
-        if (d < HD) dpv += dob[c] * bf2f(row[voff + d]);
+        if (d < HD) { qs[d] = q[c]; dos[d] = dob[c]; }
       }
-      dpv = wave_sum(dpv);
-      if (lane == 0) {
-        const bool keep = !p.p8 || sa_keep(erow + (uint32_t)j, p.p8, p.ka, p.kb);
-        pr[j] = __expf(s - lse);
-        dpr[j] = keep ? dpv * sdrop : 0.f;
-      }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < L; j += SA_THREADS) {  // one key per thread: s_j and dO . v_j
+      const bf16_t* row = qkv + (size_t)(start + j) * rs;
+      const float s = dot_q_row<HD>(qs, row + koff);
+      const float dpv = dot_q_row<HD>(dos, row + voff);
+      const bool keep = !p.p8 || sa_keep(erow + (uint32_t)j, p.p8, p.ka, p.kb);
+      pr[j] = __expf(s - lse);
+      dpr[j] = keep ? dpv * sdrop : 0.f;
     }
     __syncthreads();
     float dq[NC];

@@ -553,8 +553,13 @@ class Federation:
                 self.ledger.append(r, x["client"], x.get("kind", "update"), x["root"], x["verdict"],
                                    x.get("metrics", {}), ts=x["ts"])
             if extra is not None:
-                self.ledger.append(r, -1, extra.pop("kind", "round"), extra.pop("root", ""),
-                                   "accept", extra, ts=float(r + 1))
+                kind, root = extra.pop("kind", "round"), extra.pop("root", "")
+                if not self.collective_free and self.rt.distributed:
+                    # round-summary fields can be rank-local (async staleness, liveness view):
+                    # every rank must append the SAME block, so record all ranks' views
+                    views = D.all_gather_object(extra)
+                    extra = views[0] if all(v == views[0] for v in views) else {"per_rank": views}
+                self.ledger.append(r, -1, kind, root, "accept", extra, ts=float(r + 1))
             self.ledger.flush()
             if not self.collective_free and self.rt.distributed and not self.ledger.consensus_check():
                 raise RuntimeError(f"ledger tips diverged across ranks at round {r}")

@@ -232,3 +232,46 @@ def test_deterministic_async_is_reproducible(tmp_path):
     b = run_world(_fed_worker, 2, str(tmp_path / "b"), "serverless", str(tmp_path / "b"), kw)
     for x, y in zip(a, b):
         assert torch.equal(x["master"], y["master"])
+
+
+def _bench_path_worker(rank, world, out, kw):
+    """The bench's federation on 8 ranks (one client per rank), a few rounds."""
+    torch.set_num_threads(1)
+    from bcfl.config import get_preset
+    from bcfl.fl import Federation
+    cfg = get_preset("baseline3_learnable", model="tiny-bert", dataset="tiny", device="cpu",
+                     backend="gloo", num_rounds=3, train_samples=32, test_samples=16,
+                     global_test_samples=32, batch_size=16, max_seq_len=64, out_dir=out,
+                     reference_prints=False, save_every=1, **kw)
+    fed = Federation(cfg, verbose=False)
+    hist = fed.run()
+    res = {"master": fed.flat.master.clone(), "tip": fed.ledger.tip, "height": torch.tensor(len(fed.ledger)),
+           "loss": torch.tensor([h["train_loss"] for h in hist])}
+    if fed.ledger_audit is not None:
+        res["audit_checked"] = torch.tensor(fed.ledger_audit["checked"])
+        res["audit_mismatched"] = torch.tensor(fed.ledger_audit["mismatched"])
+    if not fed.collective_free:
+        res["consensus"] = torch.tensor(fed.ledger.consensus_check())
+    return res
+
+
+@pytest.mark.slow
+def test_bench_path_world8_mailbox(tmp_path):
+    """Exactly the bench configuration (async one-sided mailbox gossip, bf16 wire, Merkle
+    verification, drift correction, per-round checkpoints) on 8 gloo ranks: every rank finishes,
+    every accepted update matches its sender's commitment in the cross-rank ledger audit."""
+    res = run_world(_bench_path_worker, 8, str(tmp_path / "d"), str(tmp_path / "d"), {})
+    for r in res:
+        assert torch.isfinite(r["master"]).all() and torch.isfinite(r["loss"]).all()
+        assert int(r["audit_checked"]) > 0 and int(r["audit_mismatched"]) == 0
+    assert os.path.exists(tmp_path / "d" / "global" / "model.safetensors")
+
+
+@pytest.mark.slow
+def test_bench_path_world8_anomaly_filter_consensus(tmp_path):
+    """Same on 8 ranks with the update anomaly filter on (collective rounds): the hash-chained
+    ledger is identical on every rank after every round (consensus_check)."""
+    res = run_world(_bench_path_worker, 8, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"anomaly_filter": "both", "wire_dtype": "bf16"})
+    assert all(bool(r["consensus"]) for r in res)
+    assert len({r["tip"] for r in res}) == 1
