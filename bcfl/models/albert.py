@@ -87,7 +87,8 @@ class AlbertForSequenceClassification(SeqClassifierBase):
 
     def _layer(self, x, batch, rows=None):
         c, tr = self.cfg, self.training
-        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
+        t_attn, t_ffn = ops.ResidualTap(), ops.ResidualTap()   # see BertLayer.forward
+        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias, tap=t_attn if rows is None else None)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
                                        c.num_attention_heads, c.num_attention_heads, c.head_dim,
@@ -99,12 +100,12 @@ class AlbertForSequenceClassification(SeqClassifierBase):
             x = x.index_select(0, rows.long())
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.dense_weight), self.dense_bias, x,
                                             self.attn_ln_weight, self.attn_ln_bias,
-                                            c.layer_norm_eps, c.hidden_dropout_prob, tr)
-        h, pre = ops.linear_act(x1, self.ffn_weight, self.ffn_bias, c.hidden_act)
+                                            c.layer_norm_eps, c.hidden_dropout_prob, tr, tap=t_attn)
+        h, pre = ops.linear_act(x1, self.ffn_weight, self.ffn_bias, c.hidden_act, tap=t_ffn)
         y2 = ops.linear_after_act(h, pre, self.ffn_out_weight, c.hidden_act)
         return ops.bias_dropout_add_layernorm(y2, self.ffn_out_bias,
                                               x1, self.full_ln_weight, self.full_ln_bias,
-                                              c.layer_norm_eps, 0.0, tr)
+                                              c.layer_norm_eps, 0.0, tr, tap=t_ffn)
 
     def forward(self, batch: PackedBatch, token_type_ids: Optional[torch.Tensor] = None):
         c = self.cfg

@@ -75,7 +75,10 @@ class BertLayer(nn.Module):
         of the last layer; K and V still come from every token)."""
         c = self.cfg
         tr = self.training
-        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
+        # the residual gradients of both LayerNorms go straight into the dgrad GEMMs that read
+        # the same tensors (no separate gradient-sum pass; ops.ResidualTap)
+        t_attn, t_ffn = ops.ResidualTap(), ops.ResidualTap()
+        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias, tap=t_attn if rows is None else None)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
                                        c.num_attention_heads, c.num_attention_heads, c.head_dim,
@@ -88,13 +91,13 @@ class BertLayer(nn.Module):
         y = ops.linear(ctx, self.attn_out_weight)
         x1 = ops.bias_dropout_add_layernorm(y, self.attn_out_bias, x, self.attn_ln_weight,
                                             self.attn_ln_bias, c.layer_norm_eps,
-                                            c.hidden_dropout_prob, tr)
+                                            c.hidden_dropout_prob, tr, tap=t_attn)
         # dense -> GELU in one GEMM epilogue; the output GEMM's backward applies GELU' (K6)
-        h, pre = ops.linear_act(x1, self.inter_weight, self.inter_bias, c.hidden_act)
+        h, pre = ops.linear_act(x1, self.inter_weight, self.inter_bias, c.hidden_act, tap=t_ffn)
         y2 = ops.linear_after_act(h, pre, self.out_weight, c.hidden_act)
         return ops.bias_dropout_add_layernorm(y2, self.out_bias, x1, self.out_ln_weight,
                                               self.out_ln_bias, c.layer_norm_eps,
-                                              c.hidden_dropout_prob, tr)
+                                              c.hidden_dropout_prob, tr, tap=t_ffn)
 
     def hf_items(self, prefix: str):
         H = self.cfg.hidden_size

@@ -61,7 +61,8 @@ class DistilBertLayer(nn.Module):
 
     def forward(self, x, batch: PackedBatch, rows=None):
         c, tr = self.cfg, self.training
-        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
+        t_attn, t_ffn = ops.ResidualTap(), ops.ResidualTap()   # see BertLayer.forward
+        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias, tap=t_attn if rows is None else None)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
                                        c.n_heads, c.n_heads, c.head_dim, c.attention_dropout, tr)
@@ -72,12 +73,12 @@ class DistilBertLayer(nn.Module):
             x = x.index_select(0, rows.long())
         x1 = ops.bias_dropout_add_layernorm(ops.linear(ctx, self.out_lin_weight), self.out_lin_bias,
                                             x, self.sa_ln_weight, self.sa_ln_bias,
-                                            c.layer_norm_eps, 0.0, tr)
-        h, pre = ops.linear_act(x1, self.lin1_weight, self.lin1_bias, c.activation)
+                                            c.layer_norm_eps, 0.0, tr, tap=t_attn)
+        h, pre = ops.linear_act(x1, self.lin1_weight, self.lin1_bias, c.activation, tap=t_ffn)
         y2 = ops.linear_after_act(h, pre, self.lin2_weight, c.activation)
         return ops.bias_dropout_add_layernorm(y2, self.lin2_bias, x1,
                                               self.out_ln_weight, self.out_ln_bias,
-                                              c.layer_norm_eps, c.dropout, tr)
+                                              c.layer_norm_eps, c.dropout, tr, tap=t_ffn)
 
     def hf_items(self, prefix):
         H = self.cfg.dim

@@ -142,6 +142,33 @@ def _dgrad_gemm(g2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return g2.mm(w)
 
 
+class ResidualTap:
+    """Hands the residual-branch gradient of a bias-dropout-add-LayerNorm straight to the GEMM
+    that consumes the same tensor (BERT: ``x`` feeds both the QKV projection and the attention
+    LayerNorm's residual; ``x1`` feeds FFN-up and the output LayerNorm's residual).
+
+    Without it autograd receives two [T, H] gradients for that tensor and sums them in a separate
+    eager add pass. With it the LayerNorm backward parks ``dres`` here (its residual gradient is
+    returned as None) and the consumer's input-gradient GEMM accumulates into it in place
+    (``dres.addmm_(g, W)``, beta = 1 in the library epilogue): one launch and two [T, H] passes
+    fewer per layer and direction. The consumer arms the tap in its forward (it always runs
+    before the LayerNorm), and its backward always runs after the LayerNorm's (its output is
+    upstream of the LayerNorm input); an unarmed tap leaves autograd's path untouched."""
+
+    __slots__ = ("armed", "g")
+
+    def __init__(self):
+        self.armed = False
+        self.g = None
+
+
+def _dgrad_into(g2: torch.Tensor, w: torch.Tensor, tap: Optional[ResidualTap]) -> torch.Tensor:
+    if tap is not None and tap.g is not None:
+        acc, tap.g = tap.g.view(-1, w.shape[1]), None
+        return acc.addmm_(g2, w)
+    return _dgrad_gemm(g2, w)
+
+
 def _weight_grads(ctx, g2, x2, w, bias, need_w: bool, want_b: bool):
     """(dW, db) for y = x W^T + b: K9 split-M MFMA kernel (bias gradient fused in), optionally on
     the side stream (overlap) when AccumulateGrad will steal the result."""
@@ -169,8 +196,9 @@ class _Linear(torch.autograd.Function):
     (gemm.hip), optionally on a side stream (overlap)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, tap=None):
         ctx.save_for_backward(x, w)
+        ctx.tap = tap
         ctx.has_bias = b is not None
         # a parameter used several times per step gets its gradients summed by autograd on
         # autograd's stream, which a side-stream dW would race with
@@ -186,10 +214,10 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_gemm(g2, w).view(x.shape)
+            dx = _dgrad_into(g2, w, ctx.tap).view(x.shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = _weight_grads(ctx, g2, x2, w, ctx.bias, ctx.needs_input_grad[1], want_b)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _LinearAct(torch.autograd.Function):
@@ -199,27 +227,33 @@ class _LinearAct(torch.autograd.Function):
     bias+activation forward and backward passes over [T, I] disappear (K6)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, act_id):
+    def forward(ctx, x, w, b, act_id, tap=None):
         x2 = x.reshape(-1, x.shape[-1])
         h, pre = native().linear_fwd(x2, w, b, int(act_id))
         ctx.save_for_backward(x, w)
+        ctx.tap = tap
         ctx.has_bias = b is not None
         ctx.shared = getattr(w, "_bcfl_shared", False) or getattr(b, "_bcfl_shared", False)
         ctx.bias = b
         ctx.mark_non_differentiable(h)
+        # h never receives a gradient: without this autograd materialises a zero [T, N] tensor
+        # for it on every backward (a full fill pass over the FFN activation)
+        ctx.set_materialize_grads(False)
         shp = (*x.shape[:-1], w.shape[0])
         return h.view(shp), pre.view(shp)
 
     @staticmethod
     def backward(ctx, _dh, dpre):
+        if dpre is None:
+            return None, None, None, None, None
         x, w = ctx.saved_tensors
         N, K = w.shape
         g2 = dpre.reshape(-1, N)
         x2 = x.reshape(-1, K)
-        dx = _dgrad_gemm(g2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad_into(g2, w, ctx.tap).view(x.shape) if ctx.needs_input_grad[0] else None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = _weight_grads(ctx, g2, x2, w, ctx.bias, ctx.needs_input_grad[1], want_b)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class _LinearAfterAct(torch.autograd.Function):
@@ -307,18 +341,22 @@ def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0 and x.numel() // w.shape[1] >= WGRAD_MIN_ROWS)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+           tap: Optional[ResidualTap] = None) -> torch.Tensor:
     """Dense layer. GPU + bf16 + a weight that trains: :class:`_Linear` (linear.hip fwd/dgrad
     GEMMs, K9 wgrad); frozen / inference: the fused-epilogue forward GEMM alone; otherwise the
-    plain library GEMM."""
+    plain library GEMM. ``tap``: see :class:`ResidualTap`."""
     if _use_linear_fn(x, w):
-        return _Linear.apply(x, w, b)
+        if tap is not None:
+            tap.armed = True
+        return _Linear.apply(x, w, b, tap)
     if use_native(x) and not (torch.is_grad_enabled() and (w.requires_grad or x.requires_grad)):
         return _fwd_gemm(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 
 
-def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "gelu"):
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "gelu",
+               tap: Optional[ResidualTap] = None):
     """(h, pre): h = act(x W^T + b). On the GPU fast path both come out of ONE GEMM and ``pre``
     must be handed to :func:`linear_after_act` (which routes the gradient); elsewhere ``pre`` is
     None and h is an ordinary autograd tensor."""
@@ -329,8 +367,10 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act:
         if not torch.is_grad_enabled():
             h, _ = native().linear_fwd(x2, w, b, aid)
             return h.view(*x.shape[:-1], w.shape[0]), None
-        return _LinearAct.apply(x, w, b, aid)
-    return bias_act(linear(x, w), b, act), None
+        if tap is not None:
+            tap.armed = True
+        return _LinearAct.apply(x, w, b, aid, tap)
+    return bias_act(linear(x, w, tap=tap), b, act), None
 
 
 def linear_after_act(h: torch.Tensor, pre: Optional[torch.Tensor], w: torch.Tensor,
@@ -348,12 +388,13 @@ def linear_after_act(h: torch.Tensor, pre: Optional[torch.Tensor], w: torch.Tens
 # ----------------------------------------------------------------------------------------
 class _BDALN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, bias, residual, gamma, beta, eps, p8, ka, kb):
+    def forward(ctx, y, bias, residual, gamma, beta, eps, p8, ka, kb, tap=None):
         C = native()
         out, z, mean, rstd = C.bdaln_fwd(y, bias, residual, gamma, beta, float(eps), int(p8),
                                          int(ka), int(kb))
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.cfg = (p8, ka, kb, bias is not None, residual is not None, beta is not None)
+        ctx.tap = tap
         return out
 
     @staticmethod
@@ -363,15 +404,23 @@ class _BDALN(torch.autograd.Function):
         dy, dbias, dres, dgamma, dbeta = native().bdaln_bwd(dout.contiguous(), z, mean, rstd,
                                                             gamma, int(p8), int(ka), int(kb),
                                                             bool(has_b))
+        if has_r and ctx.tap is not None:
+            ctx.tap.g, dres = dres, None   # the consumer GEMM accumulates into it
         return (dy, dbias if has_b else None, dres if has_r else None, dgamma,
-                dbeta if has_beta else None, None, None, None, None)
+                dbeta if has_beta else None, None, None, None, None, None)
 
 
 def bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps: float, p: float = 0.0,
-                               training: bool = False):
+                               training: bool = False, tap: Optional[ResidualTap] = None):
+    """LayerNorm(dropout(y + bias) + residual). ``tap`` (armed by the GEMM that also reads
+    ``residual``) routes the residual gradient into that GEMM's dgrad (:class:`ResidualTap`);
+    only used with dropout on, where the kernel's residual gradient is its own buffer (p = 0
+    aliases it with dy, which the out-projection's side-stream wgrad may still be reading)."""
     p8, ka, kb = _keys(p, training)
     if use_native(y, "bdaln"):
-        return _BDALN.apply(y.contiguous(), bias, residual, gamma, beta, eps, p8, ka, kb)
+        use_tap = tap if (tap is not None and tap.armed and p8 and residual is not None
+                          and residual.requires_grad) else None
+        return _BDALN.apply(y.contiguous(), bias, residual, gamma, beta, eps, p8, ka, kb, use_tap)
     return ref.bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps, p8, ka, kb)
 
 

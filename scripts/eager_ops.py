@@ -27,6 +27,6 @@ rows = [e for e in ka if (e.key.startswith("aten::") or "Memcpy" in e.key or "co
         and dev(e) > 0]
 rows.sort(key=lambda e: -dev(e))
 print(f"{'op':40s} {'count':>7s} {'dev_us':>10s}  shapes")
-for e in rows[:60]:
+for e in rows[:160]:
     print(f"{e.key[:40]:40s} {e.count:7d} {dev(e):10.0f}  {str(e.input_shapes)[:110]}")
 fed.finish()

@@ -557,3 +557,43 @@ def test_xent_kernels_match_torch(B, C):
     want = torch.stack([2 * (lg.detach().float().argmax(-1) == lab).sum().double(),
                         torch.tensor(2.0 * B, device=DEV, dtype=torch.float64), 2 * ce, 2 * ce / B])
     torch.testing.assert_close(acc, want, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("model", ["bert-base-2l", "distilbert"])
+def test_residual_tap_matches_autograd_sum(model, monkeypatch):
+    """LayerNorm residual gradients routed into the consumer's dgrad GEMM (ops.ResidualTap,
+    beta = 1 accumulation) give the same parameter gradients as autograd's separate sum."""
+    from bcfl.data.batching import make_packed_batch
+    from bcfl.data.registry import load_split
+    from bcfl.models import build_model, special_tokens
+    import bcfl.models.bert as mb
+    import bcfl.models.distilbert as md
+    cls_id, sep_id, vocab = special_tokens(model)
+    ds = load_split("imdb", "train", vocab, 512, 1234, cls_id, sep_id)
+    b = make_packed_batch(ds, np.arange(0, 25000, 1563)[:16]).to(DEV)
+    used = []
+
+    class Rec(ops.ResidualTap):
+        __slots__ = ()
+
+        def __setattr__(self, k, v):
+            if k == "g" and v is not None:
+                used.append(1)
+            object.__setattr__(self, k, v)
+
+    grads = {}
+    for on in (False, True):
+        tap = Rec if on else (lambda: None)
+        monkeypatch.setattr(mb.ops, "ResidualTap", tap)
+        monkeypatch.setattr(md.ops, "ResidualTap", tap)
+        rng.manual_seed(7)
+        m = build_model(model, 2, device=DEV, dtype=torch.bfloat16, seed=0)
+        m.train()
+        loss = ops.cross_entropy(m(b), b.labels)
+        loss.backward()
+        ops.join_wgrad()
+        grads[on] = [p.grad.float().clone() for p in m.parameters() if p.grad is not None]
+    assert used, "no residual gradient was routed through a tap"
+    assert len(grads[False]) == len(grads[True])
+    for a, c in zip(grads[False], grads[True]):
+        assert ((a - c).norm() / a.norm().clamp_min(1e-12)) < 2e-2

@@ -51,9 +51,14 @@ def _fed_worker(rank, world, out, kw):
                    num_rounds=3, train_samples=64, test_samples=32, global_test_samples=64,
                    out_dir=out, reference_prints=False, save_every=0, device="cuda",
                    backend="gloo", async_gossip=True, gossip_transport="mailbox", **kw)
+    from bcfl.parallel import dist as D
     fed = Federation(cfg, verbose=False)
     for r in range(cfg.num_rounds):
         fed.run_round(r)
+        # test-only: round r's posts have landed before round r+1 fetches, so the accepted-update
+        # count does not depend on process timing (the protocol itself never waits)
+        fed.drain()
+        D.barrier()
     fed.finish()
     blocks = fed.ledger.blocks()
     return {"finite": torch.tensor(bool(torch.isfinite(fed.flat.master).all())),
