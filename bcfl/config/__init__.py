@@ -97,6 +97,11 @@ class FLConfig:
     resume: Optional[str] = None
     eval_local: bool = True
     eval_global: bool = True
+    overlap_global_eval: Optional[bool] = None  # score round r's model on a side stream (own
+                                          # replica + snapshot) while round r+1 trains; the
+                                          # result lands in history[r] one round later (drain()
+                                          # / finish() resolve the last one). None = auto: on for
+                                          # collective-free GPU runs of models < 1e9 parameters
     metrics_jsonl: bool = True
     reference_prints: bool = True
     log_provenance: bool = True         # per-round sampled train/test indices (reference C18)

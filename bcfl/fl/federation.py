@@ -218,6 +218,7 @@ class Federation:
         self.ckpt = AsyncCheckpointer(self.model, self.flat, cfg.async_ckpt) if (
             cfg.save_every > 0 and (self.rt.is_main or cfg.save_clients)) else None
         self.timer = PhaseTimer(sync_device=cfg.profile)
+        self._build_eval_overlap(vocab, mdtype)
         self.global_accuracies: List[float] = []
         self.history: List[dict] = []
         self.start_round = 0
@@ -564,6 +565,74 @@ class Federation:
             if not self.collective_free and self.rt.distributed and not self.ledger.consensus_check():
                 raise RuntimeError(f"ledger tips diverged across ranks at round {r}")
 
+    # ---------------- overlapped global evaluation ----------------------------------------------
+    def _build_eval_overlap(self, vocab: int, mdtype: torch.dtype):
+        """Global evaluation off the critical path: round r's evaluated model is snapshotted into
+        an eval replica (one D2D copy of the bf16 parameters) and scored on a side stream, so the
+        forward passes over the global draw run concurrently with round r+1's training (with one
+        client per GPU — the 8-GPU layout — a training step leaves most CUs idle between
+        kernels). The evaluated model, rows and kernels are exactly those of the inline path;
+        only the host read is deferred (``_resolve_eval``). Collective mode keeps the inline
+        path (its statistics are all-reduced)."""
+        cfg = self.cfg
+        self._eval_pending = None
+        self.eval_model = self.eval_flat = self.eval_trainer = self.eval_stream = None
+        on = cfg.overlap_global_eval
+        if on is None:
+            big = self.flat.numel > 1_000_000_000
+            on = self.is_cuda and self.collective_free and not big and not cfg.deterministic
+        if not (on and cfg.eval_global and self.is_cuda and self.collective_free):
+            return
+        self.eval_model = build_model(cfg.model, self.num_labels, device=self.device, dtype=mdtype,
+                                      dropout=cfg.dropout, vocab_size=vocab, seed=cfg.seed,
+                                      lora_rank=cfg.lora_rank, lora_alpha=cfg.lora_alpha)
+        _share_frozen(self.eval_model, self.model)
+        self.eval_flat = FlatParams.from_model(self.eval_model, self.device, mdtype)
+        self.eval_trainer = LocalTrainer(self.eval_model, self.eval_flat, None)
+        self.eval_stream = torch.cuda.Stream(device=self.device)
+
+    def _launch_eval_global(self, r: int) -> None:
+        """Snapshot the model the inline path would score and queue its evaluation."""
+        self._resolve_eval()
+        with self.timer.phase("eval_global"):
+            gb = self.global_test_batches(r)  # first use uploads on the current stream
+            main = torch.cuda.current_stream(self.device)
+            es = self.eval_stream
+            es.wait_stream(main)               # the mixed model and the batches are ready
+            with torch.cuda.stream(es):
+                self.eval_flat.param.copy_(self.flat.param)
+                copied = torch.cuda.Event()
+                copied.record(es)
+                # later writers of the source (next round's optimizer / mixing, issued on main
+                # or on lane streams that wait on main) are ordered after the snapshot copy
+                # only; the forward passes overlap them
+                main.wait_event(copied)
+                acc = (self.eval_trainer.evaluate_device(gb) if gb else
+                       torch.zeros(4, dtype=torch.float64, device=self.device))
+            ev = torch.cuda.Event()
+            ev.record(es)
+            self._eval_pending = (r, acc, gb, ev)
+
+    def _resolve_eval(self) -> None:
+        """Host-read a queued global evaluation and file it under its round."""
+        p, self._eval_pending = self._eval_pending, None
+        if p is None:
+            return
+        r, acc, _batches, ev = p
+        ev.synchronize()
+        a = acc.cpu().tolist()
+        ge = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+        self.global_accuracies.append(ge.accuracy)
+        if self.verbose and self.cfg.reference_prints:
+            print(f"Global Model Accuracy: {ge.accuracy * 100:.2f}%", flush=True)
+        upd = {"global_acc": ge.accuracy, "global_majority_rate": self.global_majority_rate(r),
+               "global_eval_rows": int(ge.count), "global_loss": ge.loss}
+        for rec in reversed(self.history):
+            if rec.get("round") == r:
+                rec.update(upd)
+                break
+        self.metrics.write({"round": r, "deferred_global_eval": True, **upd})
+
     def _eval_global(self, r: int) -> EvalResult:
         with self.timer.phase("eval_global"):
             gb = self.global_test_batches(r)
@@ -751,7 +820,12 @@ class Federation:
                 self.flat.rebind(self.client_master[c0], self.client_param[c0])
             else:
                 self.flat.load_master(self.client_master[c0])
-        ge = self._eval_global(r) if cfg.eval_global else None
+        ge = None
+        if cfg.eval_global:
+            if self.eval_stream is not None:
+                self._launch_eval_global(r)   # filed under round r by _resolve_eval
+            else:
+                ge = self._eval_global(r)
         loc = []
         for c, t in local_eval.items():
             a = t.cpu().tolist()
@@ -903,7 +977,8 @@ class Federation:
         return self.history
 
     def drain(self):
-        """Complete all in-flight communication (async gossip) and I/O."""
+        """Complete all in-flight communication (async gossip), evaluation and I/O."""
+        self._resolve_eval()
         if self.gossip is not None:
             self.gossip.drain()
         if self.is_cuda:

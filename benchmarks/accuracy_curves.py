@@ -35,7 +35,7 @@ CURVES = [
 def run_one(preset: str, overrides: dict, rounds: int, label: str) -> dict:
     from bcfl.fl import Federation
     from bcfl.parallel import dist as D
-    kw = {"save_every": 0, "reference_prints": False,
+    kw = {"save_every": 0, "reference_prints": False, "overlap_global_eval": False,
           "out_dir": os.path.join("runs", "curves", str(abs(hash(label)))), **overrides,
           "num_rounds": rounds}
     cfg = get_preset(preset, **kw)
