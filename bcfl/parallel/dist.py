@@ -58,7 +58,10 @@ def init_runtime(device: str = "auto", backend: str = "auto", timeout_s: int = 6
     else:
         dev = torch.device("cpu")
     if backend == "auto":
-        backend = "nccl" if use_cuda else "gloo"
+        # BCFL_DIST_BACKEND=gloo: several ranks sharing ONE GPU (RCCL refuses duplicate devices)
+        # — how the multi-rank bench path (hipIpc mailboxes between processes) is rehearsed on a
+        # 1-GPU box; the 8-GPU job uses RCCL
+        backend = os.environ.get("BCFL_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     here = False
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
