@@ -71,6 +71,11 @@ class FLConfig:
                                         # bf16 (delta-coded all-to-all + all-gather, fp32 accumulate)
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
+    micro_batches: int = 0              # a rank training ONE client at a time splits each batch into
+                                        # 2 micro-batches trained concurrently on 2 streams (second
+                                        # replica sharing the weights, gradients summed in AdamW);
+                                        # 0 = auto (= off: host-bound for BERT-base, see
+                                        # Federation._build_micro), 1 = off, 2 = on
     client_lanes: int = 0               # concurrent client lanes per rank (own replica + HIP stream);
                                         # 0 = auto: min(8, hosted) on GPU (min(2, hosted) for
                                         # models > 1e9 parameters: activation memory), 1 on CPU

@@ -423,7 +423,7 @@ void adamw(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> para
 void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
               std::vector<Tensor> grads, std::vector<int64_t> offs, double lr, double b1, double b2,
               double eps, double wd, int64_t step, int64_t mode, double grad_scale,
-              optional<Tensor> corr, double corr_lr) {
+              optional<Tensor> corr, double corr_lr, std::vector<Tensor> grads2) {
   check_cuda(master, "master");
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
               v.scalar_type() == at::kFloat, "AdamW state must be fp32");
@@ -441,6 +441,15 @@ void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
     ptrs.push_back(g.data_ptr());
     numels.push_back(g.numel());
   }
+  // grads2 (optional, same length): a second gradient per tensor (micro-batch replica), summed
+  TORCH_CHECK(grads2.empty() || grads2.size() == grads.size(), "grads2 must match grads");
+  std::vector<const void*> ptrs2;
+  for (size_t i = 0; i < grads2.size(); ++i) {
+    Tensor g = grads2[i].is_contiguous() ? grads2[i] : grads2[i].contiguous();
+    TORCH_CHECK(g.is_cuda() && dt_of(g) == gdt && g.numel() == numels[i], "grads2 shape / dtype");
+    keep.push_back(g);
+    ptrs2.push_back(g.data_ptr());
+  }
   const bool po = param_out.has_value() && param_out->defined();
   const bool hc = corr.has_value() && corr->defined();
   if (hc)
@@ -452,7 +461,7 @@ void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
                                  numels.data(), (int)ptrs.size(), gdt, (float)lr, (float)b1,
                                  (float)b2, (float)eps, (float)wd, (int)step, (int)mode,
                                  (float)grad_scale, hc ? corr->data_ptr<float>() : nullptr,
-                                 (float)corr_lr, stream()),
+                                 (float)corr_lr, stream(), ptrs2.empty() ? nullptr : ptrs2.data()),
            "adamw_mt");
 }
 

@@ -36,6 +36,9 @@
 // 0 / -1 mask + AND) instead of re-hashing in each of them.
 #include <math.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "mfma_tiles.h"
@@ -101,8 +104,11 @@ struct Stage2 {
 };
 
 // ------------------------------------------------------------------------------------------------
-template <int HD>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+// WPE: minimum waves per SIMD the register allocation must allow (1 = unconstrained: 224
+// registers, 2 waves/SIMD; 3 = 168 registers with a few spilled to scratch). Picked per launch
+// (attn_occupancy(): BCFL_ATTN_WPE, default below) so both variants can be A/B-timed in one process.
+template <int HD, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_kernel(AttnParams p) {
   constexpr int STG = 2 * TILE * HD;  // K tile | V tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);  // [2 stages][K tile | V tile]
@@ -274,8 +280,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
+template <int HD, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_dq_kernel(AttnBwdParams p) {
   constexpr int STG = 2 * TILE * HD;  // K tile (row reads for S^T, transposed for dQ) | V tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
@@ -390,8 +396,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
+template <int HD, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
   // Q | dO | lse, delta (fp32 = 2 bf16 slots) | keep words [4 waves][64 queries] (uint32)
   constexpr int STG = 2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -549,11 +555,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
 
 }  // namespace
 
+// "F,Q,K" minimum waves per SIMD of the fwd / dq / dkdv kernels (each 1 or 3; scripts/attn_time.py)
+struct AttnOcc { int f = 3, q = 1, k = 1; };  // measured: fwd 73.8 -> 70.6 us; dq, dkdv slower at 3
+const AttnOcc& attn_occupancy() {
+  static const AttnOcc o = [] {
+    AttnOcc a;
+    if (const char* e = std::getenv("BCFL_ATTN_WPE")) std::sscanf(e, "%d,%d,%d", &a.f, &a.q, &a.k);
+    return a;
+  }();
+  return o;
+}
+
 template <int HD>
 void fwd_hd(const AttnParams& p, hipStream_t s) {
   dim3 grid((p.max_s + BLK - 1) / BLK, p.nh, p.B);
   const size_t lds = (size_t)2 * 2 * TILE * HD * 2;
-  hipLaunchKernelGGL(attn_fwd_kernel<HD>, grid, dim3(256), lds, s, p);
+  if (attn_occupancy().f == 3)
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 3>), grid, dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 1>), grid, dim3(256), lds, s, p);
 }
 
 template <int HD>
@@ -565,9 +585,17 @@ void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
   const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
   hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
                      dim3(256), 0, s, dout, out, p.delta, rows);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<HD>, gq, dim3(256), (size_t)2 * 2 * TILE * HD * 2, s, p);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HD>, gk, dim3(256),
-                     (size_t)2 * (2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2) * 2, s, p);
+  const AttnOcc& o = attn_occupancy();
+  const size_t lq = (size_t)2 * 2 * TILE * HD * 2;
+  if (o.q == 3)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 3>), gq, dim3(256), lq, s, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), gq, dim3(256), lq, s, p);
+  const size_t lk = (size_t)2 * (2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2) * 2;
+  if (o.k == 3)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 3>), gk, dim3(256), lk, s, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(256), lk, s, p);
 }
 
 int attn_dropmask_words(int max_s) {

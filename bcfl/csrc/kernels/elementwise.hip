@@ -274,6 +274,7 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_kernel(
 constexpr int MT_MAX = 40;
 struct MTArgs {
   const void* g[MT_MAX];
+  const void* g2[MT_MAX];  // optional second gradient of the same tensor (micro-batch replica), summed
   int64_t off[MT_MAX];
   int64_t numel[MT_MAX];
   int64_t start[MT_MAX + 1];
@@ -319,6 +320,12 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
       float p[4], gv[4], mm[4], vv[4];
       Vec4<float>::load(master + f, p);
       Vec4<TG>::load(g, gv);
+      if (a.g2[t]) {
+        float gw[4];
+        Vec4<TG>::load(reinterpret_cast<const TG*>(a.g2[t]) + loc, gw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gv[k] += gw[k];
+      }
       Vec4<float>::load(m + f, mm);
       Vec4<float>::load(v + f, vv);
 #pragma unroll
@@ -339,8 +346,9 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
     } else {
       for (int k = 0; k < 4 && loc + k < n; ++k) {
         float p = master[f + k], mm = m[f + k], vv = v[f + k];
-        adam_elem(p, ld<TG>(g, k) * grad_scale, mm, vv, b1, b2, eps, step_size, decay_mul,
-                  denom_scale, hf);
+        float gk = ld<TG>(g, k);
+        if (a.g2[t]) gk += ld<TG>(reinterpret_cast<const TG*>(a.g2[t]) + loc, k);
+        adam_elem(p, gk * grad_scale, mm, vv, b1, b2, eps, step_size, decay_mul, denom_scale, hf);
         if (corr) p -= corr_lr * corr[f + k];
         master[f + k] = p;
         m[f + k] = mm;
@@ -559,7 +567,7 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
                     const void* const* grads, const int64_t* offs, const int64_t* numels,
                     int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
                     int step, int mode, float grad_scale, const float* corr, float corr_lr,
-                    hipStream_t s) {
+                    hipStream_t s, const void* const* grads2) {
   const double bc1 = 1.0 - __builtin_pow((double)b1, step);
   const double bc2 = 1.0 - __builtin_pow((double)b2, step);
   const int hf = mode == 0;
@@ -576,10 +584,12 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
     a.start[0] = 0;
     for (int i = 0; i < a.n; ++i) {
       a.g[i] = grads[g0 + i];
+      a.g2[i] = grads2 ? grads2[g0 + i] : nullptr;
       a.off[i] = offs[g0 + i];
       a.numel[i] = numels[g0 + i];
       a.start[i + 1] = a.start[i] + (numels[g0 + i] + 3) / 4 * 4;
-      a.aligned[i] = (((uintptr_t)grads[g0 + i]) % (4 * esz) == 0) && (offs[g0 + i] % 4 == 0);
+      a.aligned[i] = (((uintptr_t)grads[g0 + i]) % (4 * esz) == 0) && (offs[g0 + i] % 4 == 0) &&
+                     (((uintptr_t)a.g2[i]) % (4 * esz) == 0);
     }
     const int64_t total = a.start[a.n];
     if (total == 0) continue;

@@ -21,6 +21,8 @@
 // 32x32x16 accumulators; 64 reduction rows per step (4 MFMA k-steps).
 // Replaces the autograd wgrad of the reference's nn.Linear layers (HF BERT/ALBERT/DistilBERT/
 // Llama dense layers, e.g. SURVEY.md §2.6 K1 "dense GEMMs").
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "mfma_tiles.h"
@@ -240,7 +242,13 @@ int wgrad_splits(int M, int N, int K, int* Mc) {
   const int tiles = (N / BT) * (K / BT);
   // 2 workgroups fit per CU (64 KiB LDS, 2 waves/SIMD): 512 resident on 256 CUs. Never exceed
   // one full residency round — a 2nd round of a few workgroups would double the kernel time.
-  const int slots = 512;
+  // BCFL_WGRAD_SLOTS lowers the target when concurrent client lanes already fill the GPU (fewer
+  // splits = less fp32 partial traffic and a shorter reduce).
+  static const int slots = [] {
+    const char* e = std::getenv("BCFL_WGRAD_SLOTS");
+    const int v = e ? std::atoi(e) : 512;
+    return v > 0 ? v : 512;
+  }();
   int S = slots / tiles;
   const int maxS = (M + 255) / 256;  // keep >= 4 pipeline steps per split
   if (S > maxS) S = maxS;

@@ -17,7 +17,8 @@ import torch
 
 from .synthetic import TokenDataset
 
-__all__ = ["PackedBatch", "PaddedBatch", "make_packed_batch", "make_padded_batch", "ClientLoader"]
+__all__ = ["PackedBatch", "PaddedBatch", "MicroBatches", "make_packed_batch", "make_padded_batch",
+           "ClientLoader"]
 
 
 @dataclass
@@ -75,6 +76,29 @@ def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
                        max(b.max_seqlen, P), b.seq_lens, cu)
 
 
+class MicroBatches(list):
+    """One optimizer step's rows as k packed micro-batches (each padded on its own) that a
+    :class:`bcfl.fl.trainer.LocalTrainer` with micro-batch replicas trains CONCURRENTLY on k HIP
+    streams, summing the gradients into one AdamW step — how a GPU that hosts a single client
+    (8 clients on 8 GPUs) keeps more than one kernel stream busy."""
+
+    @property
+    def batch_size(self) -> int:
+        return sum(b.batch_size for b in self)
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(b.num_tokens for b in self)
+
+    @property
+    def real_tokens(self) -> int:
+        return sum(b.real_tokens for b in self)
+
+    @property
+    def labels(self) -> torch.Tensor:
+        return torch.cat([b.labels for b in self])
+
+
 @dataclass
 class PaddedBatch:
     input_ids: torch.Tensor       # [B, S] int64
@@ -120,7 +144,8 @@ class ClientLoader:
     """Epoch iterator over one client's rows (train: shuffled like ``DataLoader(shuffle=True)``)."""
 
     def __init__(self, ds: TokenDataset, indices: np.ndarray, batch_size: int = 32,
-                 shuffle: bool = False, seed: int = 0, pad_multiple: int = 0):
+                 shuffle: bool = False, seed: int = 0, pad_multiple: int = 0, split: int = 1):
+        self.split = max(1, int(split))  # > 1: every batch as MicroBatches of ~equal row counts
         self.ds = ds
         self.indices = np.asarray(indices, dtype=np.int64)
         self.batch_size = batch_size
@@ -143,10 +168,15 @@ class ClientLoader:
         r = np.random.default_rng([self.seed, e])
         return self.indices[r.permutation(len(self.indices))]
 
-    def host_batches(self, epoch: Optional[int] = None) -> List[PackedBatch]:
+    def _pack(self, idx: np.ndarray):
+        if self.split <= 1 or len(idx) < 2:
+            return pad_packed(make_packed_batch(self.ds, idx), self.pad_multiple)
+        parts = [p for p in np.array_split(idx, min(self.split, len(idx))) if len(p)]
+        return MicroBatches(pad_packed(make_packed_batch(self.ds, p), self.pad_multiple) for p in parts)
+
+    def host_batches(self, epoch: Optional[int] = None) -> list:
         order = self._order(epoch)
-        return [pad_packed(make_packed_batch(self.ds, order[i:i + self.batch_size]), self.pad_multiple)
-                for i in range(0, len(order), self.batch_size)]
+        return [self._pack(order[i:i + self.batch_size]) for i in range(0, len(order), self.batch_size)]
 
     def device_batches(self, device, epoch: Optional[int] = None) -> List[PackedBatch]:
         """All batches of one epoch, staged with ONE pinned-buffer H2D copy."""
@@ -155,28 +185,31 @@ class ClientLoader:
         dev = torch.device(device)
         if dev.type != "cuda":
             return hb
-        sizes = []
-        for b in hb:
-            sizes += [b.input_ids.numel(), b.position_ids.numel(), b.cu_seqlens.numel(),
-                      b.labels.numel()]
-        total = int(sum(sizes))
+        flat = [x for b in hb for x in (b if isinstance(b, MicroBatches) else [b])]
+        total = int(sum(b.input_ids.numel() + b.position_ids.numel() + b.cu_seqlens.numel()
+                        + b.labels.numel() for b in flat))
         host = torch.empty(total, dtype=torch.int32, pin_memory=True)
         off = 0
-        for b in hb:
+        for b in flat:
             for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
                 n = t.numel()
                 host[off:off + n].copy_(t.reshape(-1))
                 off += n
         devbuf = host.to(dev, non_blocking=True)
-        out, off = [], 0
-        for b in hb:
+        off = 0
+
+        def view(b: PackedBatch) -> PackedBatch:
+            nonlocal off
             views = []
             for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
                 n = t.numel()
                 views.append(devbuf[off:off + n])
                 off += n
-            out.append(PackedBatch(views[0], views[1], views[2], views[3], b.max_seqlen,
-                                   b.seq_lens, b.cu_host))
+            return PackedBatch(views[0], views[1], views[2], views[3], b.max_seqlen, b.seq_lens,
+                               b.cu_host)
+
+        out = [MicroBatches(view(x) for x in b) if isinstance(b, MicroBatches) else view(b)
+               for b in hb]
         self._keepalive = (host, devbuf)
         return out
 

@@ -45,7 +45,7 @@ from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
 from ..utils.obs import MetricsWriter, PhaseTimer, Telemetry
 from .drift import DriftCorrection
-from .trainer import EvalResult, LocalTrainer
+from .trainer import EvalResult, LocalTrainer, MicroReplica
 
 DATA_SEED = 1234
 
@@ -147,6 +147,7 @@ class Federation:
             for c in self.local_clients:
                 self.client_master[c] = self.flat.master.detach().clone()
         self.lanes = self._build_lanes(vocab, mdtype)
+        self._build_micro(vocab, mdtype)
         # lanes train every hosted client IN PLACE on its own resident buffers (FlatParams.rebind):
         # no per-client master copies in / out of a lane replica
         self.client_param: Dict[int, torch.Tensor] = {}
@@ -272,6 +273,33 @@ class Federation:
             lanes.append(ClientLane(i, model, flat, opt, tr, stream,
                                     list(self.local_clients[i::n])))
         return lanes
+
+    def _build_micro(self, vocab: int, mdtype: torch.dtype):
+        """Micro-batch replica for ranks that train one client at a time (e.g. 8 clients on 8
+        GPUs), whose step's kernels otherwise run one after another on one stream (13.9 ms/step
+        alone vs 9.3 ms/step per client with concurrent streams,
+        profiles/graph_capture_probe.json). Off by default: for BERT-base the two half-batch
+        passes double the host-side launch work (~7 -> ~17 ms/step) and the step becomes
+        host-bound (1-client round 0.157 -> 0.178 s, profiles/micro_batches_1client.json); it
+        pays when a step's device time dwarfs its launch cost."""
+        cfg = self.cfg
+        self.micro_split = 1
+        n = cfg.micro_batches
+        if n == 0:
+            n = 1
+        if n <= 1:
+            return
+        if n != 2:
+            raise ValueError("micro_batches must be 0 (auto), 1 or 2")
+        model = build_model(cfg.model, self.num_labels, device=self.device, dtype=mdtype,
+                            dropout=cfg.dropout, vocab_size=vocab, seed=cfg.seed,
+                            lora_rank=cfg.lora_rank, lora_alpha=cfg.lora_alpha)
+        _share_frozen(model, self.model)
+        flat = FlatParams.from_model(model, self.device, mdtype)
+        flat.rebind(self.flat.master, self.flat.param)
+        stream = torch.cuda.Stream(device=self.device) if self.is_cuda else None
+        self.trainer.micro = MicroReplica(model, flat, stream)
+        self.micro_split = 2
 
     def _on(self, lane: ClientLane):
         return torch.cuda.stream(lane.stream) if lane.stream is not None else contextlib.nullcontext()
@@ -423,7 +451,8 @@ class Federation:
     def train_batches(self, c: int, r: int, epoch: int):
         sp = self.partitions(r)[c]
         ld = ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
-                          seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple)
+                          seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple,
+                          split=self.micro_split)
         return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
 
     def _cached_batches(self, key, build):

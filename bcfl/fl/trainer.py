@@ -14,7 +14,7 @@ from typing import Dict, List, Sequence
 import torch
 
 from .. import ops
-from ..data.batching import PackedBatch
+from ..data.batching import MicroBatches, PackedBatch
 from ..parallel.flat import FlatAdamW, FlatParams
 
 
@@ -39,12 +39,59 @@ class EvalResult:
         return self.batch_mean_sum / max(self.count, 1)
 
 
+class MicroReplica:
+    """A second model instance whose parameters are views of the trainer's OWN flat buffers
+    (FlatParams.rebind), plus the HIP stream its micro-batch runs on."""
+
+    def __init__(self, model, flat: FlatParams, stream):
+        self.model, self.flat, self.stream = model, flat, stream
+
+
 class LocalTrainer:
-    def __init__(self, model, flat: FlatParams, opt: FlatAdamW):
+    def __init__(self, model, flat: FlatParams, opt: FlatAdamW, micro: "MicroReplica" = None):
         self.model, self.flat, self.opt = model, flat, opt
+        self.micro = micro
+
+    def _step_micro(self, mb: MicroBatches, loss_acc: torch.Tensor) -> None:
+        """Two micro-batches of one optimizer step trained concurrently: rows [0, B1) on the
+        current stream with this model, rows [B1, B) on the replica's stream with the replica
+        (same weights). Each loss is weighted by its share of the rows, so the summed gradient
+        is the full batch's mean-loss gradient; AdamW sums the two in its single pass."""
+        rep = self.micro
+        a, b = mb
+        B = a.batch_size + b.batch_size
+        main = torch.cuda.current_stream(self.flat.device) if self.flat.device.type == "cuda" else None
+        if rep.flat.master is not self.flat.master or rep.flat.param is not self.flat.param:
+            rep.flat.rebind(self.flat.master, self.flat.param)  # follow the main replica's rebinds
+        self.model.train()
+        rep.model.train()
+        la = ops.cross_entropy(self.model(a), a.labels) * (a.batch_size / B)
+        if main is not None:
+            rep.stream.wait_stream(main)
+            with torch.cuda.stream(rep.stream):
+                lb = ops.cross_entropy(rep.model(b), b.labels) * (b.batch_size / B)
+        else:
+            lb = ops.cross_entropy(rep.model(b), b.labels) * (b.batch_size / B)
+        la.backward()
+        if main is not None:
+            ops.join_wgrad(self.flat.device)
+            with torch.cuda.stream(rep.stream):
+                lb.backward()
+                ops.join_wgrad(self.flat.device)
+            main.wait_stream(rep.stream)
+        else:
+            lb.backward()
+        self.opt.step(partner=rep.flat)
+        self.flat.zero_grad()
+        rep.flat.zero_grad()
+        loss_acc += la.detach() + lb.detach()
 
     def step(self, b: PackedBatch, loss_acc: torch.Tensor) -> None:
         """One optimizer step on one batch; the loss is accumulated on the device (no sync)."""
+        if isinstance(b, MicroBatches):
+            if self.micro is not None and len(b) == 2:
+                return self._step_micro(b, loss_acc)
+            raise ValueError("micro-batches need a LocalTrainer with a micro replica (2 parts)")
         self.model.train()
         logits = self.model(b)
         loss = ops.cross_entropy(logits, b.labels)

@@ -35,20 +35,26 @@ def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], 
                  lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
                  mode: str = "hf", param_out: Optional[torch.Tensor] = None,
                  grad_scale: float = 1.0, corr: Optional[torch.Tensor] = None,
-                 corr_lr: float = 0.0):
+                 corr_lr: float = 0.0, grads2: Optional[Sequence[torch.Tensor]] = None):
     """AdamW where each gradient is its own tensor (as autograd produced it) and master / m / v /
     param live in flat buffers at ``offsets``: one multi-tensor launch per <=40 tensors.
 
     ``corr`` (flat fp32, optional): drift correction in update space, applied in the same pass as
-    ``p -= corr_lr * corr`` on every element that received a gradient (bcfl.fl.drift)."""
+    ``p -= corr_lr * corr`` on every element that received a gradient (bcfl.fl.drift).
+    ``grads2`` (optional, aligned with ``grads``): a second gradient of each tensor — the
+    micro-batch replica's — summed in the same pass (no separate accumulation kernel)."""
     if not grads:
         return
+    if grads2 is not None and len(grads2) != len(grads):
+        raise ValueError("grads2 must align with grads")
     if use_native(master, "adamw"):
         native().adamw_mt(master, m, v, param_out, list(grads), [int(o) for o in offsets],
                           float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
                           int(step), 0 if mode == "hf" else 1, float(grad_scale), corr,
-                          float(corr_lr))
+                          float(corr_lr), list(grads2) if grads2 is not None else [])
         return
+    if grads2 is not None:
+        grads = [g + g2 for g, g2 in zip(grads, grads2)]
     for g, o in zip(grads, offsets):
         n = g.numel()
         po = None if param_out is None or param_out.data_ptr() == master.data_ptr() else param_out[o:o + n]

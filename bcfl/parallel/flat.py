@@ -142,15 +142,29 @@ class FlatAdamW:
         self.step_count = 0
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0):
+    def step(self, grad_scale: float = 1.0, partner: Optional[FlatParams] = None):
+        """One AdamW step. ``partner``: a micro-batch replica bound to the SAME buffers whose
+        parameters hold the gradient of the other rows of the batch; both gradients are summed
+        inside the multi-tensor kernel."""
         self.step_count += 1
         f = self.flat
-        grads, offs = f.grads()
+        grads2 = None
+        if partner is None:
+            grads, offs = f.grads()
+        else:
+            grads, offs, grads2 = [], [], []
+            for p, q, (o, n, shp) in zip(f.params, partner.params, f.slots):
+                g1, g2 = p.grad, q.grad
+                if g1 is None and g2 is None:
+                    continue
+                grads.append(g1 if g1 is not None else torch.zeros_like(g2))
+                grads2.append(g2 if g2 is not None else torch.zeros_like(g1))
+                offs.append(o)
         ops.adamw_multi_(f.master, grads, offs, self.m, self.v, self.step_count, self.lr,
                          self.betas[0], self.betas[1], self.eps, self.wd, self.mode,
                          param_out=None if f.master is f.param else f.param,
                          grad_scale=grad_scale, corr=self.corr,
-                         corr_lr=self.lr * self.corr_scale)
+                         corr_lr=self.lr * self.corr_scale, grads2=grads2)
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}

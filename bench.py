@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
     ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
+    ap.add_argument("--micro-batches", type=int, default=0,
+                    help="ranks training one client at a time: 2 = concurrent micro-batches, 1 = off, 0 = auto")
     return ap.parse_args()
 
 
@@ -97,7 +99,7 @@ def main():
                      **({} if a.lr is None else {"lr": a.lr}),
                      async_gossip=not a.sync, ledger=not a.no_ledger,
                      save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
-                     device=a.device, client_lanes=a.lanes,
+                     device=a.device, client_lanes=a.lanes, micro_batches=a.micro_batches,
                      overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad))
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
@@ -164,6 +166,7 @@ def main():
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
                        "client_lanes_per_gpu": len(fed.lanes) or 1,
+                       "micro_batches_per_step": fed.micro_split,
                        "overlap_wgrad": ops.wgrad_overlap_enabled(),
                        "checkpoint_every_round": cfg.save_every == 1 and ck is not None
                                                  and ck.skipped == 0,

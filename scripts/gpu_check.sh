@@ -20,5 +20,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
 f=$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)
 python3 "$ROOT/scripts/summarize_prof.py" "$f" "bench $TAG" > "$OUT/kernel_stats.md"
 cp "$f" "$OUT/kernel_stats.csv"
+t=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
+[ -n "$t" ] && python3 "$ROOT/scripts/busy_union.py" "$t" > "$OUT/busy.json"
 rm -rf "$OUT/prof"  # full traces exceed gpurun's 64 MiB copy-back
 head -30 "$OUT/kernel_stats.md"

@@ -295,3 +295,34 @@ def test_noniid_label_shards_learn_with_drift_correction(tmp_path, mode):
         D.set_runtime_for_tests(None)
     assert hist[-1]["global_majority_rate"] == 0.5
     assert max(h["global_acc"] for h in hist[-3:]) > 0.8, [h["global_acc"] for h in hist]
+
+
+def test_micro_batch_step_matches_full_batch():
+    """A step split into two concurrently-trained micro-batches (second replica bound to the same
+    flat buffers, row-share-weighted losses, gradients summed inside AdamW) equals the full-batch
+    step (dropout off; fp32 CPU: summation order only)."""
+    import numpy as np
+    from bcfl.data.batching import ClientLoader, MicroBatches
+    from bcfl.data.registry import load_split
+    from bcfl.fl.trainer import LocalTrainer, MicroReplica
+    from bcfl.models import build_model
+    from bcfl.parallel.flat import FlatAdamW, FlatParams
+    ds = load_split("tiny", "train", 2048, 128)
+    outs = []
+    for split in (1, 2):
+        m = build_model("tiny-bert", 2, seed=0, dropout=0.0)
+        flat = FlatParams.from_model(m, "cpu", torch.float32)
+        tr = LocalTrainer(m, flat, FlatAdamW(flat, 1e-3))
+        if split == 2:
+            m2 = build_model("tiny-bert", 2, seed=1, dropout=0.0)   # weights replaced by rebind
+            f2 = FlatParams.from_model(m2, "cpu", torch.float32)
+            f2.rebind(flat.master, flat.param)
+            tr.micro = MicroReplica(m2, f2, None)
+        batches = ClientLoader(ds, np.arange(0, 70), 32, shuffle=True, seed=3,
+                               split=split).host_batches(0)
+        assert all(isinstance(b, MicroBatches) for b in batches) == (split == 2)
+        res = tr.train_epoch(batches)
+        outs.append((flat.master.clone(), float(res["loss_sum"]), res["examples"], res["tokens"]))
+    assert outs[0][2:] == outs[1][2:]
+    assert outs[1][1] == pytest.approx(outs[0][1], rel=1e-6)
+    assert float((outs[0][0] - outs[1][0]).abs().max()) < 1e-6

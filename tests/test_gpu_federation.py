@@ -137,3 +137,29 @@ def test_gpu_overlapped_global_eval_matches_inline(tmp_path):
     assert b_loss == pytest.approx(a_loss, rel=1e-4)
     # concurrent evaluation can only reorder library reductions of the training GEMMs
     assert float((a_m - b_m).abs().max()) < 2e-4
+
+
+def test_gpu_micro_batch_clients_match_full_batch(tmp_path):
+    """Server mode trains one client at a time: with micro_batches=2 (2 concurrent micro-batches
+    on 2 streams) the run tracks the full-batch run (dropout off; bf16 gradient sums round
+    differently, so compare losses / parameters, not bits)."""
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    outs = []
+    for mb in (1, 2):
+        D.set_runtime_for_tests(None)
+        cfg = FLConfig(mode="server", model="bert-base-2l", dataset="imdb", num_clients=2,
+                       num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                       out_dir=str(tmp_path / str(mb)), reference_prints=False, save_every=0,
+                       dropout=0.0, micro_batches=mb, overlap_wgrad=False)
+        fed = Federation(cfg, verbose=False)
+        assert fed.micro_split == (1 if mb == 1 else 2)
+        h = fed.run()
+        outs.append(([r["train_loss"] for r in h], [r["global_acc"] for r in h],
+                     fed.global_master.cpu()))
+        D.set_runtime_for_tests(None)
+    (la, aa, ma), (lb, ab, mb_) = outs
+    assert lb == pytest.approx(la, rel=2e-2)
+    assert torch.isfinite(mb_).all()
+    assert float((ma - mb_).abs().max()) < 5e-3

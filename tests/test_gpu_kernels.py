@@ -597,3 +597,27 @@ def test_residual_tap_matches_autograd_sum(model, monkeypatch):
     assert len(grads[False]) == len(grads[True])
     for a, c in zip(grads[False], grads[True]):
         assert ((a - c).norm() / a.norm().clamp_min(1e-12)) < 2e-2
+
+
+def test_multi_tensor_adamw_sums_second_gradient():
+    """adamw_mt with grads2 == adamw_mt on (g1 + g2) (micro-batch replicas' gradients)."""
+    torch.manual_seed(0)
+    shapes = [(768, 768), (3072,), (33,)]
+    offs, o = [], 0
+    for s in shapes:
+        offs.append(o)
+        o += (math.prod(s) + 63) // 64 * 64
+    g1 = [torch.randn(s, device=DEV).bfloat16() for s in shapes]
+    g2 = [torch.randn(s, device=DEV).bfloat16() for s in shapes]
+    gs = [(a.float() + b.float()).bfloat16() for a, b in zip(g1, g2)]
+    res = []
+    for grads, grads2 in ((g1, g2), (gs, None)):
+        torch.manual_seed(1)
+        master = torch.randn(o, device=DEV)
+        m_, v_ = torch.zeros(o, device=DEV), torch.zeros(o, device=DEV)
+        ops.adamw_multi_(master, grads, offs, m_, v_, 1, 1e-3, 0.9, 0.999, 1e-6, 0.0, "hf",
+                         grads2=grads2)
+        res.append((master, m_, v_))
+    # g1 + g2 in fp32 inside the kernel vs a bf16-rounded sum: m differs by bf16 rounding only
+    for a, b in zip(res[0], res[1]):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)) < 1e-2
