@@ -53,8 +53,11 @@ class FLConfig:
     adam_eps: float = 1e-6
     adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
     keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
-    drift_correction: str = "none"      # none | scaffold (control variates in update space,
-                                        # fused into AdamW; no extra communication — fl/drift.py)
+    drift_correction: str = "none"      # none | scaffold | auto (control variates in update
+                                        # space, fused into AdamW; no extra communication —
+                                        # fl/drift.py). auto = scaffold for label-skewed
+                                        # partitions (label_shards, ref_contiguous, dirichlet),
+                                        # none for IID ones
     drift_correction_scale: float = 1.0
     dropout: Optional[float] = None     # None -> model default
     dtype: str = "bf16"                 # compute dtype on GPU ("bf16" | "fp32")
@@ -132,7 +135,7 @@ class FLConfig:
                    "topology": ("full", "ring", "pagerank"),
                    "gossip_transport": ("auto", "mailbox", "rccl"),
                    "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
-                   "drift_correction": ("none", "scaffold"), "adam_mode": ("hf", "torch"),
+                   "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
                    "fedavg_weighting": ("examples", "batches", "uniform")}
@@ -262,16 +265,17 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # The reference fine-tunes PRETRAINED checkpoints at lr 5e-5 with a fresh AdamW per round
     # (server_IID_IMDB.py:109). From random init a 12-layer post-LN BERT does not leave the
     # constant-prediction plateau at that rate; the measured protocol that learns (MI355X sweeps,
-    # profiles/accuracy_curves_*.json): lr 2e-5 with 3 rounds of linear warm-up, AdamW moments kept
-    # per client across rounds, and a synthetic task whose planted class tokens are 12 per 64.
+    # profiles/accuracy_curves_*.json): lr 2e-5 with 3 rounds of linear warm-up, the reference's
+    # fresh AdamW per round, and a synthetic task whose planted class tokens are 12 per 64.
     # Label-sharded clients (one class each) additionally need client-drift correction
     # (SCAFFOLD control variates, bcfl/fl/drift.py): without it the mixed model collapses to the
-    # majority rate after every local epoch.
+    # majority rate after every local epoch. IID partitions train better without it
+    # (profiles/accuracy_curves_iid_mi355x.json), hence drift_correction="auto".
     "baseline3_learnable": dict(mode="serverless", model="bert-base", dataset="imdb", num_labels=2,
                                 num_clients=8, num_rounds=20, partition="label_shards",
                                 train_samples=240, test_samples=60, async_gossip=True, lr=2e-5,
                                 lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
-                                global_test_samples=1000, drift_correction="scaffold"),
+                                global_test_samples=1000, drift_correction="auto"),
     "baseline4_biobert_serverless_noniid_trust": dict(mode="serverless", model="biobert",
                                                       dataset="imdb", num_labels=2, num_clients=8,
                                                       num_rounds=20, partition="label_shards",

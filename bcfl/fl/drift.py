@@ -36,6 +36,16 @@ import torch
 from .. import ops
 
 MODES = ("none", "scaffold")
+# partitions whose clients see skewed label distributions (bcfl/data/partition.py)
+LABEL_SKEWED = ("label_shards", "ref_contiguous", "dirichlet")
+
+
+def resolve_mode(mode: str, partition: str) -> str:
+    """``auto``: SCAFFOLD where local optima disagree (label-skewed shards), off for IID splits,
+    where the control variates only add noise (profiles/accuracy_curves_iid_mi355x.json)."""
+    if mode == "auto":
+        return "scaffold" if partition in LABEL_SKEWED else "none"
+    return mode
 
 
 class DriftCorrection:

@@ -44,7 +44,7 @@ from ..parallel.topology import clients_of_rank, mixing_matrix, neighbours
 from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
 from ..utils.obs import MetricsWriter, PhaseTimer, Telemetry
-from .drift import DriftCorrection
+from .drift import DriftCorrection, resolve_mode as resolve_drift
 from .trainer import EvalResult, LocalTrainer, MicroReplica
 
 DATA_SEED = 1234
@@ -156,7 +156,8 @@ class Federation:
                 self.client_param[c] = torch.empty(self.flat.numel, dtype=self.flat.dtype,
                                                    device=self.device)
                 ops.cast_copy_(self.client_param[c], self.client_master[c])
-        self.drift = DriftCorrection(cfg.drift_correction, cfg.drift_correction_scale,
+        self.drift = DriftCorrection(resolve_drift(cfg.drift_correction, cfg.partition),
+                                     cfg.drift_correction_scale,
                                      self.local_clients, self.flat.numel, self.device)
         ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else len(self.lanes) <= 1
         if cfg.deterministic:

@@ -154,7 +154,7 @@ def main():
                                   "lr_warmup_steps": cfg.lr_warmup_steps,
                                   "keep_optimizer_state": cfg.keep_optimizer_state,
                                   "synthetic_signal": cfg.synthetic_signal,
-                                  "drift_correction": cfg.drift_correction,
+                                  "drift_correction": fed.drift.mode,
                                   "rounds_trained": a.warmup + a.steps},
             "tokens_per_s": tokens / dt,
             "samples_per_s": a.clients * cfg.train_samples * a.steps / dt,

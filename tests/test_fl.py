@@ -287,8 +287,9 @@ def test_noniid_label_shards_learn_with_drift_correction(tmp_path, mode):
                          train_samples=256, global_test_samples=200, eval_local=False,
                          save_every=0, ledger=False, device="cpu", reference_prints=False,
                          out_dir=str(tmp_path))
-        assert cfg.partition == "label_shards" and cfg.drift_correction == "scaffold"
+        assert cfg.partition == "label_shards" and cfg.drift_correction == "auto"
         fed = Federation(cfg, verbose=False)
+        assert fed.drift.mode == "scaffold"     # auto resolves to SCAFFOLD on label shards
         hist = fed.run()
     finally:
         torch.set_num_threads(nt)
@@ -326,3 +327,12 @@ def test_micro_batch_step_matches_full_batch():
     assert outs[0][2:] == outs[1][2:]
     assert outs[1][1] == pytest.approx(outs[0][1], rel=1e-6)
     assert float((outs[0][0] - outs[1][0]).abs().max()) < 1e-6
+
+
+def test_drift_correction_auto_resolution():
+    from bcfl.fl.drift import resolve_mode
+    assert resolve_mode("auto", "label_shards") == "scaffold"
+    assert resolve_mode("auto", "dirichlet") == "scaffold"
+    assert resolve_mode("auto", "iid_random") == "none"
+    assert resolve_mode("scaffold", "iid_random") == "scaffold"
+    assert resolve_mode("none", "label_shards") == "none"
