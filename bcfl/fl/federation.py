@@ -23,6 +23,7 @@ import json
 import math
 import os
 import time
+import warnings
 import zlib
 from dataclasses import dataclass, field
 from typing import Dict, Iterator, List, Optional
@@ -40,6 +41,7 @@ from ..models import build_model, model_config, special_tokens
 from ..parallel import dist as D
 from ..parallel.flat import FlatAdamW, FlatParams
 from ..parallel.gossip import GossipEngine, MailboxGossip
+from ..parallel.mailbox import MailboxUnavailable
 from ..parallel.topology import clients_of_rank, mixing_matrix, neighbours
 from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
@@ -189,12 +191,20 @@ class Federation:
             states = ({c: self.client_master[c] for c in self.local_clients} if self.multi
                       else {self.local_clients[0]: self.flat.master})
             if self.transport == "mailbox":
-                self.gossip = MailboxGossip(n, states, self.nbrs,
-                                            "fp32" if cfg.wire_dtype == "fp32" else "bf16",
-                                            sync=not cfg.async_gossip,
-                                            liveness_timeout=cfg.liveness_timeout,
-                                            verify=cfg.verify_updates)
-            else:
+                try:
+                    self.gossip = MailboxGossip(n, states, self.nbrs,
+                                                "fp32" if cfg.wire_dtype == "fp32" else "bf16",
+                                                sync=not cfg.async_gossip,
+                                                liveness_timeout=cfg.liveness_timeout,
+                                                verify=cfg.verify_updates)
+                except MailboxUnavailable as e:
+                    # every rank sees the same outcome (agreed collectively in the transport):
+                    # fall back together to the lock-step RCCL engine
+                    warnings.warn(f"hipIpc mailboxes unavailable ({e}); gossip falls back to "
+                                  "RCCL send/recv (lock-step)", RuntimeWarning)
+                    self.transport = "rccl"
+                    self.collective_free = False
+            if self.transport != "mailbox":
                 wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
                 if cfg.wire_dtype == "bf16_raw":
                     wire = "bf16"

@@ -142,6 +142,11 @@ class _Box:
         self._keep = (hdr_raw, pay_raw)
 
 
+class MailboxUnavailable(RuntimeError):
+    """Raised on EVERY rank when any rank could not allocate, export or map its inboxes (the
+    outcome is agreed collectively, so all ranks can fall back to the RCCL engine together)."""
+
+
 class MailboxTransport:
     """Inboxes for ``listen`` (remote clients this rank reads) and mapped peer inboxes for
     ``send_plan`` ((local client, destination rank) pairs). Construction is collective (one
@@ -161,19 +166,33 @@ class MailboxTransport:
         self.pay_bytes = 2 * _align(self.payload_bytes)
         self.backend = HipIpcBackend(device) if self.is_cuda else ShmBackend(f"r{self.rank}")
         self.inbox: Dict[int, _Box] = {}
-        handles = {}
-        for j in listen:
-            h, hh = self.backend.alloc(self.hdr_bytes, f"h{j}")
-            p, ph = self.backend.alloc(self.pay_bytes, f"p{j}")
-            self.inbox[j] = _Box(h, p, numel, dtype)
-            handles[j] = (hh, ph)
-        table = D.all_gather_object(handles)  # the only collective: handle exchange at start-up
+        handles, err = {}, None
+        try:
+            for j in listen:
+                h, hh = self.backend.alloc(self.hdr_bytes, f"h{j}")
+                p, ph = self.backend.alloc(self.pay_bytes, f"p{j}")
+                self.inbox[j] = _Box(h, p, numel, dtype)
+                handles[j] = (hh, ph)
+        except Exception as e:  # reported collectively below, never left half-joined
+            err = f"rank {self.rank} inbox allocation / export: {e!r}"
+        # start-up handle exchange (with each rank's allocation outcome)
+        table = D.all_gather_object({"handles": handles, "err": err})
         self.outbox: Dict[int, List[Tuple[int, _Box]]] = {}
-        for c, dst in send_plan:
-            hh, ph = table[dst][c]
-            box = _Box(self.backend.open(hh, self.hdr_bytes), self.backend.open(ph, self.pay_bytes),
-                       numel, dtype)
-            self.outbox.setdefault(c, []).append((dst, box))
+        if err is None and not any(t["err"] for t in table):
+            try:
+                for c, dst in send_plan:
+                    hh, ph = table[dst]["handles"][c]
+                    box = _Box(self.backend.open(hh, self.hdr_bytes),
+                               self.backend.open(ph, self.pay_bytes), numel, dtype)
+                    self.outbox.setdefault(c, []).append((dst, box))
+            except Exception as e:
+                err = f"rank {self.rank} peer mapping: {e!r}"
+        errs = [e for e in D.all_gather_object(err) if e] + [t["err"] for t in table if t["err"]]
+        if errs:
+            self.outbox.clear()
+            self.inbox.clear()
+            self.backend.release_names()
+            raise MailboxUnavailable("; ".join(sorted(set(errs))))
         self.streams = ({d: torch.cuda.Stream(device=device) for d in {d for _, d in send_plan}}
                         if self.is_cuda else {})
         # every peer has mapped its destinations: shared-memory names can go now (mappings stay

@@ -143,3 +143,28 @@ def test_mailbox_exited_peer_does_not_stall(tmp_path):
     assert int(res[1]["exited"]) == 1
     assert len(res[0]["times"]) == 6
     assert res[0]["dead"].tolist() == [1]
+
+
+def _fallback_worker(rank, world, out):
+    from bcfl.fl import Federation
+    from bcfl.parallel import mailbox as mb
+    if rank == 1:  # this rank cannot map its peers' inboxes
+        def bad_open(self, handle, nbytes):
+            raise OSError("simulated hipIpcOpenMemHandle failure")
+        mb.ShmBackend.open = bad_open
+    fed = Federation(_cfg(out), verbose=False)
+    for r in range(fed.cfg.num_rounds):
+        fed.run_round(r)
+    fed.finish(audit=False)
+    return {"transport_rccl": torch.tensor(int(fed.transport == "rccl")),
+            "collective_free": torch.tensor(int(fed.collective_free)),
+            "finite": torch.tensor(int(torch.isfinite(fed.flat.master).all()))}
+
+
+def test_mailbox_failure_on_one_rank_falls_back_to_rccl_everywhere(tmp_path):
+    """A mapping failure on ONE rank is agreed collectively: every rank gets MailboxUnavailable
+    and the federation continues on the lock-step RCCL (here gloo) engine instead of hanging."""
+    res = run_world(_fallback_worker, 2, str(tmp_path), str(tmp_path / "fb"))
+    for r in res:
+        assert int(r["transport_rccl"]) == 1 and int(r["collective_free"]) == 0
+        assert int(r["finite"]) == 1
