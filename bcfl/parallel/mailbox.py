@@ -202,6 +202,10 @@ class MailboxTransport:
         self.posted: Dict[Tuple[int, int], List["torch.cuda.Event"]] = {}  # (client, slot)
         self.torn = 0
         self.bytes_posted = 0
+        # measured peer-copy times (GPU): the payload copy of every post is bracketed by timing
+        # events on its side stream — the information-passing time over xGMI, measured in the run
+        self._timed: List[Tuple[int, "torch.cuda.Event", "torch.cuda.Event"]] = []
+        self._post_ms: List[Tuple[int, float]] = []
 
     # ------------------------------------------------------------------ sender
     def wait_slot_free(self, c: int, slot: int):
@@ -231,7 +235,11 @@ class MailboxTransport:
                 st.wait_event(ready)
                 with torch.cuda.stream(st):
                     self.backend.hdr_store(box.hdr, slot, [snap.version], W_BEGIN)
+                    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    t0.record(st)
                     box.slots[slot].copy_(payload, non_blocking=True)
+                    t1.record(st)
+                    self._timed.append((dst, t0, t1))
                     if root_dev is not None:
                         box.hdr[slot, W_ROOT:W_ROOT + 4].copy_(root_dev.view(torch.int64),
                                                                non_blocking=True)
@@ -249,7 +257,30 @@ class MailboxTransport:
         if evs:
             self.posted[(c, slot)] = evs
 
+    def _collect_timings(self):
+        keep = []
+        for dst, t0, t1 in self._timed:
+            if t1.query():
+                self._post_ms.append((dst, t0.elapsed_time(t1)))
+            else:
+                keep.append((dst, t0, t1))
+        self._timed = keep
+        del self._post_ms[:-512]  # recent posts only
+
+    def post_stats(self) -> Optional[Dict[str, float]]:
+        """Measured payload-copy time per post (ms) and the implied per-destination bandwidth
+        (GB/s): the information-passing time of one model update to one peer."""
+        self._collect_timings()
+        if not self._post_ms:
+            return None
+        ms = np.array([m for _, m in self._post_ms])
+        return {"posts": int(ms.size), "payload_mb": self.payload_bytes / 1e6,
+                "ms_median": float(np.median(ms)), "ms_max": float(ms.max()),
+                "gb_per_s_median": float(self.payload_bytes / np.median(ms) / 1e6),
+                "destinations": int(len({d for d, _ in self._post_ms}))}
+
     def drain(self):
+        self._collect_timings()
         for evs in self.posted.values():
             for ev in evs:
                 ev.synchronize()

@@ -129,6 +129,10 @@ def main():
     s_per_round = dt / a.steps
     phases = {k: v for k, v in last.items() if k.startswith("t_")}
     ck = fed.ckpt
+    # measured peer-copy times of the mailbox posts (multi-rank runs: one model update to one
+    # peer over xGMI), read before finish() closes the transport
+    tr = getattr(fed.gossip, "transport", None)
+    p2p = tr.post_stats() if tr is not None and hasattr(tr, "post_stats") else None
     fed.finish()
     if rt.is_main:
         rec = {
@@ -172,6 +176,7 @@ def main():
                                                  and ck.skipped == 0,
                        "gossip_transport": fed.transport},
             "checkpoints": {"saved": ck.saved if ck else 0, "skipped": ck.skipped if ck else 0},
+            "p2p_post_measured": p2p,
             "ledger": {"height": len(fed.ledger) if fed.ledger else 0,
                        "audit": fed.ledger_audit,
                        "rejected_msgs": last.get("rejected_msgs")},
