@@ -36,7 +36,7 @@ def med(fn, n=30):
     return float(np.median(ts))
 
 
-p8, ka, kb = 26, 12345, 678
+p8, ka, kb = int(os.environ.get("P8", "26")), 12345, 678
 out, lse, mask = C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb)
 g = torch.randn_like(out)
 tf_ = med(lambda: C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb))
