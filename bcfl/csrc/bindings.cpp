@@ -299,7 +299,8 @@ std::vector<Tensor> emb_ln_fwd(Tensor ids, Tensor pos, optional<Tensor> tt, Tens
 // the parameter dtype — no fp32 [V, H] buffer, no atomics, no cast pass.
 std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Tensor> tt, Tensor z,
                                Tensor mean, Tensor rstd, Tensor gamma, int64_t V, int64_t P,
-                               int64_t TV, int64_t p8, int64_t ka, int64_t kb) {
+                               int64_t TV, int64_t p8, int64_t ka, int64_t kb,
+                               optional<Tensor> ord_ids, optional<Tensor> ord_pos) {
   check_cuda(dout, "dout");
   const int T = ids.numel(), H = z.size(1);
   const int dt = dt_of(z);
@@ -316,6 +317,19 @@ std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Ten
                                   (uint32_t)kb, tsum ? 1 : 0, dt, stream(), /*drop_in=*/1),
            "emb_ln_bwd");
   auto piece = torch::empty({T, H}, f);
+  // ord: [2, T] int32 (stable-sorted keys | source rows), precomputed on the host with the batch
+  // (ClientLoader presort) — no device sort per step; otherwise sorted here
+  auto table_grad_ord = [&](const Tensor& ord, int64_t rows) {
+    TORCH_CHECK(ord.is_cuda() && ord.scalar_type() == at::kInt && ord.dim() == 2 &&
+                ord.size(0) == 2 && ord.size(1) == T && ord.is_contiguous(),
+                "emb_ln_bwd: order must be a contiguous int32 [2, T] device tensor");
+    auto g = torch::zeros({rows, H}, popt);
+    const int* o = ord.data_ptr<int>();
+    check_rc(bcfl::launch_segment_rowsum_i32(dx.data_ptr(), dt, o, o + T, piece.data_ptr<float>(),
+                                             g.data_ptr(), dt, T, H, stream()),
+             "segment_rowsum");
+    return g;
+  };
   auto table_grad = [&](const Tensor& key32, int64_t rows) {
     auto g = torch::zeros({rows, H}, popt);
     auto sorted = at::sort(key32.to(torch::kLong), /*stable=*/true, /*dim=*/0, /*descending=*/false);
@@ -327,8 +341,10 @@ std::vector<Tensor> emb_ln_bwd(Tensor dout, Tensor ids, Tensor pos, optional<Ten
              "segment_rowsum");
     return g;
   };
-  Tensor dword = table_grad(ids, V);
-  Tensor dpos = P > 0 ? table_grad(pos, P) : Tensor();
+  const bool oi = ord_ids.has_value() && ord_ids->defined();
+  const bool op = ord_pos.has_value() && ord_pos->defined();
+  Tensor dword = oi ? table_grad_ord(*ord_ids, V) : table_grad(ids, V);
+  Tensor dpos = P > 0 ? (op ? table_grad_ord(*ord_pos, P) : table_grad(pos, P)) : Tensor();
   Tensor dtype_;
   if (TV > 0) dtype_ = ttp ? table_grad(*tt, TV) : torch::zeros({TV, H}, popt);
   auto dgamma = torch::empty({H}, popt), dbeta = torch::empty({H}, popt);

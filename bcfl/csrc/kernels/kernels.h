@@ -22,6 +22,8 @@ int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const f
 // deterministic); piece: fp32 [T, H] scratch
 int launch_segment_rowsum(const void* src, int src_dt, const int64_t* keys, const int64_t* perm,
                           float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s);
+int launch_segment_rowsum_i32(const void* src, int src_dt, const int* keys, const int* perm,
+                              float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s);
 int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,
                   hipStream_t s);
 // reduce planes 0..2 of partial[nblk][3][H] into out0..2 (nullptr = skip) in one launch

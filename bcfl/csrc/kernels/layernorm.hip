@@ -220,10 +220,10 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
 // Fixed summation order throughout, so the result is bitwise reproducible.
 constexpr int SEG_C = 16;
 
-template <typename TA, int NCH>
+template <typename TA, int NCH, typename IT>
 __global__ __launch_bounds__(256) void segment_pass1_kernel(const TA* __restrict__ src,
-                                                            const int64_t* __restrict__ keys,
-                                                            const int64_t* __restrict__ perm,
+                                                            const IT* __restrict__ keys,
+                                                            const IT* __restrict__ perm,
                                                             float* __restrict__ piece, int T, int H) {
   const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int p0 = chunk * SEG_C;
@@ -283,9 +283,9 @@ __global__ __launch_bounds__(256) void segment_pass1_kernel(const TA* __restrict
   flush(head);
 }
 
-template <typename TD>
+template <typename TD, typename IT>
 __global__ __launch_bounds__(256) void segment_pass2_kernel(const float* __restrict__ piece,
-                                                            const int64_t* __restrict__ keys,
+                                                            const IT* __restrict__ keys,
                                                             TD* __restrict__ dst, int T, int H) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= T) return;
@@ -957,25 +957,40 @@ int launch_bdaln_bwd(const void* dout, const void* z, const float* mean, const f
   return 0;
 }
 
-int launch_segment_rowsum(const void* src, int src_dt, const int64_t* keys, const int64_t* perm,
-                          float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s) {
+namespace {
+template <typename IT>
+int segment_rowsum_t(const void* src, int src_dt, const IT* keys, const IT* perm, float* piece,
+                     void* dst, int dst_dt, int T, int H, hipStream_t s) {
   if (T <= 0) return 0;
   if (H % 4) return -2;
   dim3 g1(((T + SEG_C - 1) / SEG_C + 3) / 4), g2((T + 3) / 4);
   if (src_dt == DT_BF16) {
-    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<bf16_t, NC>), g1, dim3(256), 0, s,
+    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<bf16_t, NC, IT>), g1, dim3(256), 0, s,
                                              (const bf16_t*)src, keys, perm, piece, T, H));
   } else {
-    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<float, NC>), g1, dim3(256), 0, s,
+    NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((segment_pass1_kernel<float, NC, IT>), g1, dim3(256), 0, s,
                                              (const float*)src, keys, perm, piece, T, H));
   }
   if (dst_dt == DT_BF16)
-    hipLaunchKernelGGL((segment_pass2_kernel<bf16_t>), g2, dim3(256), 0, s, piece, keys,
+    hipLaunchKernelGGL((segment_pass2_kernel<bf16_t, IT>), g2, dim3(256), 0, s, piece, keys,
                        (bf16_t*)dst, T, H);
   else
-    hipLaunchKernelGGL((segment_pass2_kernel<float>), g2, dim3(256), 0, s, piece, keys, (float*)dst,
-                       T, H);
+    hipLaunchKernelGGL((segment_pass2_kernel<float, IT>), g2, dim3(256), 0, s, piece, keys,
+                       (float*)dst, T, H);
   return 0;
+}
+
+}  // namespace
+
+int launch_segment_rowsum(const void* src, int src_dt, const int64_t* keys, const int64_t* perm,
+                          float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s) {
+  return segment_rowsum_t<int64_t>(src, src_dt, keys, perm, piece, dst, dst_dt, T, H, s);
+}
+
+// keys / perm precomputed on the host (int32, stable order): no device sort per step
+int launch_segment_rowsum_i32(const void* src, int src_dt, const int* keys, const int* perm,
+                              float* piece, void* dst, int dst_dt, int T, int H, hipStream_t s) {
+  return segment_rowsum_t<int>(src, src_dt, keys, perm, piece, dst, dst_dt, T, H, s);
 }
 
 int launch_colsum(const float* partial, int nblk, int nk_stride, int k, int H, void* out, int dt,

@@ -30,6 +30,14 @@ class PackedBatch:
     max_seqlen: int
     seq_lens: np.ndarray        # host copy of row lengths (real rows only)
     cu_host: np.ndarray         # host copy of cu_seqlens (incl. the filler row, if any)
+    # optional [2, T] int32 stable sort orders (sorted keys | source rows) of input_ids and
+    # position_ids, computed on the host with the batch (ClientLoader presort): the embedding
+    # table gradients then need no device sort per step
+    sort_ids: Optional[torch.Tensor] = None
+    sort_pos: Optional[torch.Tensor] = None
+
+    def order(self):
+        return (self.sort_ids, self.sort_pos) if self.sort_ids is not None else None
 
     @property
     def batch_size(self) -> int:
@@ -49,11 +57,23 @@ class PackedBatch:
         return int(self.cu_host[self.batch_size])
 
     def to(self, device, non_blocking: bool = True) -> "PackedBatch":
-        return PackedBatch(self.input_ids.to(device, non_blocking=non_blocking),
-                           self.position_ids.to(device, non_blocking=non_blocking),
-                           self.cu_seqlens.to(device, non_blocking=non_blocking),
-                           self.labels.to(device, non_blocking=non_blocking),
-                           self.max_seqlen, self.seq_lens, self.cu_host)
+        mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
+        return PackedBatch(mv(self.input_ids), mv(self.position_ids), mv(self.cu_seqlens),
+                           mv(self.labels), self.max_seqlen, self.seq_lens, self.cu_host,
+                           mv(self.sort_ids), mv(self.sort_pos))
+
+
+def _sort_order(keys: torch.Tensor) -> torch.Tensor:
+    """[2, T] int32: stable ascending sort of ``keys`` (sorted keys | source positions) — the
+    same order the device path's stable at::sort produces."""
+    k = keys.numpy()
+    perm = np.argsort(k, kind="stable")
+    return torch.from_numpy(np.stack([k[perm], perm]).astype(np.int32))
+
+
+def presort(b: PackedBatch) -> PackedBatch:
+    return PackedBatch(b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.max_seqlen,
+                       b.seq_lens, b.cu_host, _sort_order(b.input_ids), _sort_order(b.position_ids))
 
 
 def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
@@ -144,8 +164,10 @@ class ClientLoader:
     """Epoch iterator over one client's rows (train: shuffled like ``DataLoader(shuffle=True)``)."""
 
     def __init__(self, ds: TokenDataset, indices: np.ndarray, batch_size: int = 32,
-                 shuffle: bool = False, seed: int = 0, pad_multiple: int = 0, split: int = 1):
+                 shuffle: bool = False, seed: int = 0, pad_multiple: int = 0, split: int = 1,
+                 presort: bool = False):
         self.split = max(1, int(split))  # > 1: every batch as MicroBatches of ~equal row counts
+        self.presort = presort           # training batches: host-side embedding sort orders
         self.ds = ds
         self.indices = np.asarray(indices, dtype=np.int64)
         self.batch_size = batch_size
@@ -168,11 +190,15 @@ class ClientLoader:
         r = np.random.default_rng([self.seed, e])
         return self.indices[r.permutation(len(self.indices))]
 
+    def _one(self, idx: np.ndarray) -> PackedBatch:
+        b = pad_packed(make_packed_batch(self.ds, idx), self.pad_multiple)
+        return presort(b) if self.presort else b
+
     def _pack(self, idx: np.ndarray):
         if self.split <= 1 or len(idx) < 2:
-            return pad_packed(make_packed_batch(self.ds, idx), self.pad_multiple)
+            return self._one(idx)
         parts = [p for p in np.array_split(idx, min(self.split, len(idx))) if len(p)]
-        return MicroBatches(pad_packed(make_packed_batch(self.ds, p), self.pad_multiple) for p in parts)
+        return MicroBatches(self._one(p) for p in parts)
 
     def host_batches(self, epoch: Optional[int] = None) -> list:
         order = self._order(epoch)
@@ -186,12 +212,16 @@ class ClientLoader:
         if dev.type != "cuda":
             return hb
         flat = [x for b in hb for x in (b if isinstance(b, MicroBatches) else [b])]
-        total = int(sum(b.input_ids.numel() + b.position_ids.numel() + b.cu_seqlens.numel()
-                        + b.labels.numel() for b in flat))
+
+        def parts(b: PackedBatch):
+            return [t for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.sort_ids,
+                                b.sort_pos) if t is not None]
+
+        total = int(sum(t.numel() for b in flat for t in parts(b)))
         host = torch.empty(total, dtype=torch.int32, pin_memory=True)
         off = 0
         for b in flat:
-            for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
+            for t in parts(b):
                 n = t.numel()
                 host[off:off + n].copy_(t.reshape(-1))
                 off += n
@@ -201,12 +231,13 @@ class ClientLoader:
         def view(b: PackedBatch) -> PackedBatch:
             nonlocal off
             views = []
-            for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels):
+            for t in parts(b):
                 n = t.numel()
-                views.append(devbuf[off:off + n])
+                views.append(devbuf[off:off + n].view(t.shape))
                 off += n
+            so = (views[4], views[5]) if b.sort_ids is not None else (None, None)
             return PackedBatch(views[0], views[1], views[2], views[3], b.max_seqlen, b.seq_lens,
-                               b.cu_host)
+                               b.cu_host, *so)
 
         out = [MicroBatches(view(x) for x in b) if isinstance(b, MicroBatches) else view(b)
                for b in hb]

@@ -463,7 +463,7 @@ class Federation:
         sp = self.partitions(r)[c]
         ld = ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
                           seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple,
-                          split=self.micro_split)
+                          split=self.micro_split, presort=self.is_cuda)
         return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
 
     def _cached_batches(self, key, build):

@@ -114,7 +114,7 @@ class AlbertForSequenceClassification(SeqClassifierBase):
                                     self.word_embeddings, self.position_embeddings,
                                     self.token_type_embeddings, self.emb_ln_weight,
                                     self.emb_ln_bias, c.layer_norm_eps, c.hidden_dropout_prob,
-                                    self.training)
+                                    self.training, order=batch.order())
         x = ops.linear(e, self.map_weight, self.map_bias)
         rows = batch.cu_seqlens[:batch.n_seq]
         for i in range(c.num_hidden_layers):

@@ -151,7 +151,7 @@ class BertForSequenceClassification(SeqClassifierBase):
                                     self.word_embeddings, self.position_embeddings,
                                     self.token_type_embeddings, self.emb_ln_weight,
                                     self.emb_ln_bias, c.layer_norm_eps, c.hidden_dropout_prob,
-                                    self.training)
+                                    self.training, order=batch.order())
         last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):
             x = layer(x, batch, rows if i == last else None)

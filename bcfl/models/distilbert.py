@@ -126,7 +126,7 @@ class DistilBertForSequenceClassification(SeqClassifierBase):
         check_positions(batch, c.max_position_embeddings)
         x = ops.embedding_layernorm(batch.input_ids, batch.position_ids, None, self.word_embeddings,
                                     self.position_embeddings, None, self.emb_ln_weight,
-                                    self.emb_ln_bias, c.layer_norm_eps, c.dropout, self.training)
+                                    self.emb_ln_bias, c.layer_norm_eps, c.dropout, self.training, order=batch.order())
         rows = batch.cu_seqlens[:batch.n_seq]
         last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):

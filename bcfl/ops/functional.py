@@ -572,12 +572,14 @@ def query_subset_attention(qkv: torch.Tensor, rows: torch.Tensor, cu_seqlens: to
 # ----------------------------------------------------------------------------------------
 class _EmbLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8, ka, kb):
+    def forward(ctx, ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8, ka, kb,
+                ord_ids=None, ord_pos=None):
         C = native()
         out, z, mean, rstd = C.emb_ln_fwd(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma,
                                           beta, float(eps), int(p8), int(ka), int(kb))
         ctx.save_for_backward(ids, pos_ids, type_ids, z, mean, rstd, gamma, word_w, pos_w, type_w)
         ctx.cfg = (p8, ka, kb)
+        ctx.order = (ord_ids, ord_pos)
         return out
 
     @staticmethod
@@ -588,19 +590,24 @@ class _EmbLN(torch.autograd.Function):
         dword, dpos, dtype_, dgamma, dbeta = C.emb_ln_bwd(
             dout.contiguous(), ids, pos_ids, type_ids, z, mean, rstd, gamma, int(word_w.shape[0]),
             int(pos_w.shape[0]) if pos_w is not None else 0,
-            int(type_w.shape[0]) if type_w is not None else 0, int(p8), int(ka), int(kb))
+            int(type_w.shape[0]) if type_w is not None else 0, int(p8), int(ka), int(kb),
+            *ctx.order)
         return (None, None, None, dword.to(word_w.dtype),
                 dpos.to(pos_w.dtype) if pos_w is not None else None,
                 dtype_.to(type_w.dtype) if type_w is not None else None,
-                dgamma, dbeta, None, None, None, None)
+                dgamma, dbeta, None, None, None, None, None, None)
 
 
 def embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps: float,
-                        p: float = 0.0, training: bool = False):
+                        p: float = 0.0, training: bool = False, order=None):
+    """Embedding gather-sum + LayerNorm (+ dropout). ``order``: the batch's host-precomputed
+    (ids, positions) stable sort orders, int32 [2, T] each (``PackedBatch.sort_ids`` /
+    ``sort_pos``) — the table gradients then need no device sort."""
     p8, ka, kb = _keys(p, training)
     if use_native(word_w, "emb_ln"):
+        oi, op = order if order is not None else (None, None)
         return _EmbLN.apply(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta, eps, p8,
-                            ka, kb)
+                            ka, kb, oi, op)
     return ref.embedding_layernorm(ids, pos_ids, type_ids, word_w, pos_w, type_w, gamma, beta,
                                    eps, p8, ka, kb)
 

@@ -621,3 +621,29 @@ def test_multi_tensor_adamw_sums_second_gradient():
     # g1 + g2 in fp32 inside the kernel vs a bf16-rounded sum: m differs by bf16 rounding only
     for a, b in zip(res[0], res[1]):
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)) < 1e-2
+
+
+def test_embedding_grads_with_host_sort_order_are_identical():
+    """Table gradients from the host-precomputed stable sort orders (ClientLoader presort) are
+    bitwise identical to the device-sort path."""
+    from bcfl.data.batching import make_packed_batch, pad_packed, presort
+    from bcfl.data.registry import load_split
+    torch.manual_seed(0)
+    ds = load_split("imdb", "train", 30522, 512)
+    b = presort(pad_packed(make_packed_batch(ds, np.arange(0, 25000, 997)[:24]), 256)).to(DEV)
+    assert b.sort_ids.shape == (2, b.num_tokens) and b.sort_ids.dtype == torch.int32
+    H = 768
+    word = (0.02 * torch.randn(30522, H, device=DEV)).bfloat16().requires_grad_(True)
+    posw = (0.02 * torch.randn(512, H, device=DEV)).bfloat16().requires_grad_(True)
+    typ = (0.02 * torch.randn(2, H, device=DEV)).bfloat16().requires_grad_(True)
+    g = torch.ones(H, device=DEV).bfloat16().requires_grad_(True)
+    be = torch.zeros(H, device=DEV).bfloat16().requires_grad_(True)
+    go = torch.randn(b.num_tokens, H, device=DEV).bfloat16()
+    outs = []
+    for order in (None, b.order()):
+        rng.manual_seed(3)
+        y = ops.embedding_layernorm(b.input_ids, b.position_ids, None, word, posw, typ, g, be,
+                                    1e-12, 0.1, True, order=order)
+        outs.append(torch.autograd.grad(y, (word, posw, typ, g, be), go))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
