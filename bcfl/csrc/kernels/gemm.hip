@@ -205,10 +205,22 @@ __global__ __launch_bounds__(TPB) void wgrad_kernel(WgradParams p) {
     }
 }
 
-// out[n, k] = bf16( sum_s part[s, n, k] ), fixed summation order (deterministic)
+// out[n, k] = bf16( sum_s part[s, n, k] ), fixed summation order (deterministic). The blocks
+// past the main grid reduce the bias-gradient partials db[n] = bf16( sum_s dbias_part[s, n] ) in
+// the same launch (one reduction kernel per weight gradient instead of two).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int S,
                                                            int N, int K, bf16_t* __restrict__ out,
-                                                           int64_t ldo) {
+                                                           int64_t ldo, int main_blocks,
+                                                           const float* __restrict__ bpart,
+                                                           bf16_t* __restrict__ dbias) {
+  if ((int)blockIdx.x >= main_blocks) {  // bias columns (block-uniform branch)
+    const int n = (blockIdx.x - main_blocks) * 256 + threadIdx.x;
+    if (n >= N) return;
+    float a = 0.f;
+    for (int s = 0; s < S; ++s) a += bpart[(int64_t)s * N + n];
+    dbias[n] = f2bf(a);
+    return;
+  }
   const int64_t NK = (int64_t)N * K;
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (e >= NK) return;
@@ -223,16 +235,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const int64_t n = e / K, k = e - n * K;
   const float v[4] = {a.x, a.y, a.z, a.w};
   Vec4<bf16_t>::store(out + n * ldo + k, v);
-}
-
-// db[n] = bf16( sum_s part[s, n] )
-__global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* __restrict__ part, int S,
-                                                                int N, bf16_t* __restrict__ out) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float a = 0.f;
-  for (int s = 0; s < S; ++s) a += part[(int64_t)s * N + n];
-  out[n] = f2bf(a);
 }
 
 }  // namespace
@@ -269,11 +271,11 @@ int launch_wgrad(const WgradParams& p, hipStream_t s) {
     hipLaunchKernelGGL(wgrad_kernel<false>, dim3(tiles * p.S), dim3(TPB), lds, s, p);
   if (p.S > 1) {
     const int64_t n4 = (int64_t)p.N * p.K / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                       p.part, p.S, p.N, p.K, reinterpret_cast<bf16_t*>(p.out), p.ldo);
-    if (p.dbias_part)
-      hipLaunchKernelGGL(wgrad_bias_reduce_kernel, dim3((p.N + 255) / 256), dim3(256), 0, s,
-                         p.dbias_part, p.S, p.N, reinterpret_cast<bf16_t*>(p.dbias));
+    const int main_blocks = (int)((n4 + 255) / 256);
+    const int bias_blocks = p.dbias_part ? (p.N + 255) / 256 : 0;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(main_blocks + bias_blocks)), dim3(256),
+                       0, s, p.part, p.S, p.N, p.K, reinterpret_cast<bf16_t*>(p.out), p.ldo,
+                       main_blocks, p.dbias_part, reinterpret_cast<bf16_t*>(p.dbias));
   }
   return 0;
 }
