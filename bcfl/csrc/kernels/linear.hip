@@ -24,6 +24,8 @@
 // of 128 and K of 64 (every BERT / ALBERT / DistilBERT / Llama projection); the host falls back
 // to the library GEMM otherwise. The workgroup -> tile map is XCD-aware (bijective for any grid):
 // each XCD walks a contiguous range of row-major tiles, so the A rows it streams stay in its L2.
+#include <cstdlib>
+
 #include "act.h"
 #include "common.h"
 #include "kernels.h"
@@ -311,6 +313,211 @@ __global__ __launch_bounds__(64 * WGM * WGN) void linear_kernel(LinearParams p) 
   }
 }
 
+// Persistent variant of the 128 x 128 kernel: a grid of at most 2 workgroups per CU walks the
+// tiles (stride = grid size, a multiple of 8 so every tile keeps its XCD), and the first two
+// reduction steps of the NEXT tile are loaded before the current tile's epilogue, so their
+// latency hides behind the epilogue (with K = 768 a tile has only 12 steps; prologue and epilogue
+// are a large share of it). Default for the 128 x 128 configuration (same-box A/B at the bench
+// shapes: dgrad +4..9 %, GELU' dgrad +2..5 %, forward +0..4 %, fused bias+GELU forward unchanged;
+// profiles/experiments_r2.md); BCFL_LINEAR_PERSIST=0 selects the one-tile-per-workgroup kernel.
+template <bool NN, int EPI, int ACT>
+__global__ __launch_bounds__(256) void linear_persist_kernel(LinearParams p) {
+  constexpr int BM = 128, BN = 128, WGN = 2, T = 256;
+  constexpr int WTM = 64, WTN = 64, I = 2, J = 2;
+  constexpr int A_E = BM * LK, B_E = BN * LK, STG = A_E + B_E;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tilesN = p.N / BN;
+  const int tilesM = (p.M + BM - 1) / BM;
+  const int nwg = tilesM * tilesN;
+  const int G = gridDim.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  auto remap = [&](int t) {  // bijective XCD-aware map (t & 7 = this workgroup's XCD)
+    const int xcd = t & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+  };
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / WGN, wn = w % WGN;
+  const int hh = lane >> 5;
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* B = reinterpret_cast<const bf16_t*>(p.B);
+  const int nsteps = p.K / LK;
+
+  int offa[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) offa[ks] = swz_off<LK>(WTM * wm + (lane & 31), 2 * ks + hh);
+  int offb[4];
+  int offbt[J][2];
+  if constexpr (!NN) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) offb[ks] = swz_off<LK>(WTN * wn + (lane & 31), 2 * ks + hh);
+  } else {
+    const int g16 = (lane >> 4) & 1, q = (lane & 15) >> 2, pc = lane & 3;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int u = WTN / 32 * wn + j;
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+        const int row = 4 * hh + q + 8 * hi;
+        offbt[j][hi] = (u >> 2) * (64 * 128) +
+                       swz_off<128>(row, 4 * (u & 3) + 2 * g16 + (pc >> 1)) + 4 * (pc & 1);
+      }
+    }
+  }
+  const int va = (threadIdx.x >> 3) * (int)p.lda * 2 + (threadIdx.x & 7) * 16;
+  const int ra_row = T / 8 * (int)p.lda * 2;
+  using ATile = RowTile<BM, T>;
+  using BTileT = typename std::conditional<NN, ColTile<BN, T>, RowTile<BN, T>>::type;
+  // per-tile operand sources (A rows m0.., B rows n0.. (NT) or columns n0.. (NN))
+  struct Src {
+    __amdgpu_buffer_rsrc_t ra, rb;
+    int vb;
+  };
+  const int rb_row = NN ? (int)p.ldb * 2 : T / 8 * (int)p.ldb * 2;
+  const int rb_step = NN ? LK * (int)p.ldb * 2 : LK * 2;
+  const __amdgpu_buffer_rsrc_t rb_nn = rows_rsrc_l(B, p.ldb, 0, p.K);
+  auto source = [&](int L) {
+    Src sr;
+    const int m0 = (L / tilesN) * BM, n0 = (L % tilesN) * BN;
+    sr.ra = rows_rsrc_l(A, p.lda, m0, min(p.M, m0 + BM));
+    if constexpr (!NN) {
+      sr.rb = rows_rsrc_l(B, p.ldb, n0, n0 + BN);
+      sr.vb = (threadIdx.x >> 3) * (int)p.ldb * 2 + (threadIdx.x & 7) * 16;
+    } else {
+      sr.rb = rb_nn;
+      sr.vb = (threadIdx.x >> 4) * (int)p.ldb * 2 + (n0 + (threadIdx.x & 15) * 8) * 2;
+    }
+    return sr;
+  };
+  auto load_a = [&](ATile& t, const Src& sr, int step) { t.load(sr.ra, va, ra_row, step * LK * 2); };
+  auto load_b = [&](BTileT& t, const Src& sr, int step) { t.load(sr.rb, sr.vb, rb_row, step * rb_step); };
+
+  f32x16_t acc[I][J];
+  auto compute = [&](int it) {
+    const bf16_t* As = lds + (it & 1) * STG;
+    const bf16_t* Bs = As + A_E;
+#pragma unroll
+    for (int ks = 0; ks < LK / 16; ++ks) {
+      bf16x8_t fa[I], fb[J];
+#pragma unroll
+      for (int i = 0; i < I; ++i) fa[i] = lds_row8(As + offa[ks] + 32 * i * LK);
+      if constexpr (!NN) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) fb[j] = lds_row8(Bs + offb[ks] + 32 * j * LK);
+      } else {
+#pragma unroll
+        for (int j = 0; j < J; ++j) fb[j] = tr_operand(Bs + 16 * ks * 128, offbt[j][0], offbt[j][1]);
+      }
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+  };
+
+  int tile = blockIdx.x;
+  int L = remap(tile);
+  Src cur = source(L);
+  ATile a0, a1;
+  BTileT b0, b1;
+  load_a(a0, cur, 0);
+  load_b(b0, cur, 0);
+  load_a(a1, cur, 1);
+  load_b(b1, cur, 1);
+  const bf16_t* bias = reinterpret_cast<const bf16_t*>(p.bias);
+  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  bf16_t* aux = reinterpret_cast<bf16_t*>(p.aux);
+  float* ep = reinterpret_cast<float*>(smem) + w * (32 * EP_LD);
+  const int cc = (lane & 7) * 8;
+
+  while (true) {  // workgroup-uniform trip count
+    const int m0 = (L / tilesN) * BM, n0 = (L % tilesN) * BN;
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j) acc[i][j] = zero16();
+    a0.store(lds);
+    b0.store(lds + A_E);
+    __syncthreads();
+    auto step = [&](int it, ATile& al, BTileT& bl, ATile& as, BTileT& bs) {
+      load_a(al, cur, it + 2);
+      load_b(bl, cur, it + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(it);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16_t* nx = lds + ((it + 1) & 1) * STG;
+      as.store(nx);
+      bs.store(nx + A_E);
+      __syncthreads();
+    };
+    int it = 0;
+    for (; it + 1 < nsteps; it += 2) {
+      step(it, a0, b0, a1, b1);
+      step(it + 1, a1, b1, a0, b0);
+    }
+    if (nsteps & 1) compute(it);
+    // next tile's first two steps go in flight now, under this tile's epilogue
+    const int next = tile + G;
+    const bool more = next < nwg;
+    int Ln = L;
+    Src nsr = cur;
+    if (more) {
+      Ln = remap(next);
+      nsr = source(Ln);
+      load_a(a0, nsr, 0);
+      load_b(b0, nsr, 0);
+      load_a(a1, nsr, 1);
+      load_b(b1, nsr, 1);
+    }
+    // ---- epilogue (as linear_kernel) ----
+    const int n = n0 + WTN * wn + cc;
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ACT) {
+      if (bias) Vec8<bf16_t>::load(bias + n, bv);
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          ep[acc_row(reg, hh) * EP_LD + 32 * j + (lane & 31)] = acc[i][j][reg];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 3) + 8 * r;
+        const int m = m0 + WTM * wm + 32 * i + rr;
+        if (m < p.M) {
+          float v[8];
+          Vec8<float>::load(ep + rr * EP_LD + cc, v);
+          if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bv[e];
+          } else if constexpr (EPI == EPI_BIAS_ACT) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] + bv[e]));
+            Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + n, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = act_ft<ACT>(v[e]);
+          } else if constexpr (EPI == EPI_DACT) {
+            float a[8];
+            Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, a);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= act_dt<ACT>(a[e]);
+          }
+          Vec8<bf16_t>::store(C + (int64_t)m * p.ldc + n, v);
+        }
+      }
+    }
+    if (!more) break;
+    __syncthreads();  // every wave's slab reads are done before stage 0 is overwritten
+    tile = next;
+    L = Ln;
+    cur = nsr;
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN>
 constexpr size_t lin_lds() {
   const size_t stages = (size_t)2 * (BM + BN) * LK * sizeof(bf16_t);
@@ -347,6 +554,35 @@ int launch_cfg(const LinearParams& p, hipStream_t s) {
 }
 
 template <bool NN>
+int launch_persist(const LinearParams& p, hipStream_t s) {
+  const int nwg = ((p.M + 127) / 128) * (p.N / 128);
+  const int slots = 512;  // 2 workgroups per CU x 256 CUs; a multiple of 8 (tile keeps its XCD)
+  const int g = nwg < slots ? nwg : slots;
+  constexpr size_t lds = lin_lds<128, 128, 2, 2>();
+#define BCFL_LINP(E, A) \
+  hipLaunchKernelGGL((linear_persist_kernel<NN, E, A>), dim3(g), dim3(256), lds, s, p)
+  if (p.epi == EPI_STORE) {
+    BCFL_LINP(EPI_STORE, 0);
+  } else if (p.epi == EPI_BIAS) {
+    BCFL_LINP(EPI_BIAS, 0);
+  } else if (p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) {
+    const bool fwd = p.epi == EPI_BIAS_ACT;
+    switch (p.act) {
+      case ACT_GELU: if (fwd) BCFL_LINP(EPI_BIAS_ACT, ACT_GELU); else BCFL_LINP(EPI_DACT, ACT_GELU); break;
+      case ACT_GELU_TANH:
+        if (fwd) BCFL_LINP(EPI_BIAS_ACT, ACT_GELU_TANH); else BCFL_LINP(EPI_DACT, ACT_GELU_TANH);
+        break;
+      case ACT_RELU: if (fwd) BCFL_LINP(EPI_BIAS_ACT, ACT_RELU); else BCFL_LINP(EPI_DACT, ACT_RELU); break;
+      default: return -5;
+    }
+  } else {
+    return -4;
+  }
+#undef BCFL_LINP
+  return 0;
+}
+
+template <bool NN>
 int launch_linear_t(const LinearParams& p, hipStream_t s) {
   if (p.N % 128 || p.K % LK || p.M < 0 || p.K <= 0) return -1;
   if (p.lda % 8 || p.ldb % 8 || p.ldc % 8 || p.ldaux % 8) return -2;
@@ -362,6 +598,11 @@ int launch_linear_t(const LinearParams& p, hipStream_t s) {
     tile = (p.N % 256 == 0 && p.K >= 2048 && t256 >= 240) ? 1 : 0;
   }
   if (tile == 1 && p.N % 256 == 0) return launch_cfg<NN, 256, 256, 2, 4>(p, s);
+  static const bool persist = [] {
+    const char* e = std::getenv("BCFL_LINEAR_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  if (persist) return launch_persist<NN>(p, s);
   return launch_cfg<NN, 128, 128, 2, 2>(p, s);
 }
 
