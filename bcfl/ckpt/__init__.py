@@ -84,6 +84,25 @@ def save_dir(out_dir: str, model, flat_host: np.ndarray, layout, config: Dict[st
         json.dump(config, fh, indent=2, sort_keys=True)
 
 
+def link_dir(src_dir: str, out_dir: str, config: Dict[str, Any]):
+    """``out_dir`` gets the weights ``save_dir`` just wrote to ``src_dir`` (hard link, or a copy
+    across filesystems). Writers replace files (tmp + rename), so a later save never changes a
+    linked file in place."""
+    os.makedirs(out_dir, exist_ok=True)
+    src = os.path.join(src_dir, "model.safetensors")
+    dst = os.path.join(out_dir, "model.safetensors")
+    tmp = dst + ".tmp"
+    if os.path.lexists(tmp):
+        os.remove(tmp)
+    try:
+        os.link(src, tmp)
+    except OSError:
+        shutil.copyfile(src, tmp)
+    os.replace(tmp, dst)
+    with open(os.path.join(out_dir, "config.json"), "w") as fh:
+        json.dump(config, fh, indent=2, sort_keys=True)
+
+
 def dir_size_gb(path: str) -> float:
     """Reference ``get_dir_size`` (os.walk sum; E5's getsize-on-a-directory bug fixed)."""
     tot = 0
@@ -138,6 +157,18 @@ class AsyncCheckpointer:
             return False
         if jobs is None:
             jobs = [(out_dirs, self.flat.master if master is None else master)]
+        # jobs whose source is the same buffer (a 1-client rank's global model IS its client
+        # model) are copied and serialised once; the other dirs get a hard link to the file
+        merged: List[tuple] = []
+        by_src: Dict[Tuple[int, int], int] = {}
+        for k, (dirs, src) in enumerate(jobs):
+            key = (src.data_ptr(), src.numel())
+            if key in by_src:
+                merged[by_src[key]][0].extend((d, k == 0) for d in dirs)
+            else:
+                by_src[key] = len(merged)
+                merged.append(([(d, k == 0) for d in dirs], src))
+        jobs = merged
         bufs = [self._buf(i) for i in range(len(jobs))]
         if self.cuda:
             cur = torch.cuda.current_stream(self.stream.device)
@@ -156,11 +187,16 @@ class AsyncCheckpointer:
         def _write():
             if done is not None:
                 done.synchronize()
-            for k, (b, (dirs, _)) in enumerate(zip(bufs, jobs)):
+            for b, (dirs, _) in zip(bufs, jobs):
                 host = b.numpy()
-                for d in dirs:
-                    save_dir(d, self.model, host, self.layout, self.config, metadata)
-                    if state is not None and k == 0:
+                first = None
+                for d, with_state in dirs:
+                    if first is None:
+                        save_dir(d, self.model, host, self.layout, self.config, metadata)
+                        first = d
+                    else:
+                        link_dir(first, d, self.config)
+                    if state is not None and with_state:
                         with open(os.path.join(d, "state.json"), "w") as fh:
                             json.dump(state, fh, indent=2, sort_keys=True, default=str)
             for path, obj in (extra_files or {}).items():
@@ -169,7 +205,7 @@ class AsyncCheckpointer:
                 os.replace(path + ".tmp", path)
             with self._lock:
                 self.saved += 1
-                self.last_dir = jobs[0][0][0] if jobs and jobs[0][0] else None
+                self.last_dir = jobs[0][0][0][0] if jobs and jobs[0][0] else None
 
         if self.async_:
             self.future = self.pool.submit(_write)

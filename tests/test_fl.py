@@ -336,3 +336,28 @@ def test_drift_correction_auto_resolution():
     assert resolve_mode("auto", "iid_random") == "none"
     assert resolve_mode("scaffold", "iid_random") == "scaffold"
     assert resolve_mode("none", "label_shards") == "none"
+
+
+def test_checkpoint_jobs_sharing_a_source_are_written_once(tmp_out):
+    """A 1-client rank's global model and client model are one buffer: serialised once, the
+    second dir gets a link to the same bytes; state.json only goes to the first job's dirs."""
+    from bcfl.ckpt import AsyncCheckpointer, read_safetensors
+    fed = Federation(_cfg(tmp_out, mode="serverless", num_rounds=1, save_every=0), verbose=False)
+    ck = AsyncCheckpointer(fed.model, fed.flat, async_=False)
+    other = fed.flat.master * 2.0
+    d = [os.path.join(tmp_out, x) for x in ("g", "c0", "c1")]
+    assert ck.save([], state={"round": 0}, jobs=[([d[0]], fed.flat.master), ([d[1]], fed.flat.master),
+                                                 ([d[2]], other)])
+    assert len(ck.pinned) == 2  # one host copy per distinct source
+    sd = [read_safetensors(os.path.join(x, "model.safetensors")) for x in d]
+    for k in sd[0]:
+        assert torch.equal(sd[0][k], sd[1][k])
+        assert torch.equal(sd[2][k], sd[0][k] * 2.0)
+    assert os.path.exists(os.path.join(d[0], "state.json"))
+    assert not os.path.exists(os.path.join(d[1], "state.json"))
+    assert all(os.path.exists(os.path.join(x, "config.json")) for x in d)
+    # the next save replaces the linked file instead of writing through the link
+    fed.flat.master.add_(1.0)
+    ck.save([], jobs=[([d[0]], fed.flat.master), ([d[1]], fed.flat.master)])
+    sd2 = read_safetensors(os.path.join(d[1], "model.safetensors"))
+    assert not torch.equal(sd2[next(iter(sd2))], sd[1][next(iter(sd2))])
