@@ -187,6 +187,12 @@ class AsyncCheckpointer:
         def _write():
             if done is not None:
                 done.synchronize()
+            st = state
+            if st is not None and callable(st.get("_finalize")):
+                # fields only known once device work queued before the save has finished (e.g. an
+                # overlapped evaluation of this round): resolved here, on the writer thread
+                st = dict(st)
+                st.update(st.pop("_finalize")())
             for b, (dirs, _) in zip(bufs, jobs):
                 host = b.numpy()
                 first = None
@@ -196,9 +202,9 @@ class AsyncCheckpointer:
                         first = d
                     else:
                         link_dir(first, d, self.config)
-                    if state is not None and with_state:
+                    if st is not None and with_state:
                         with open(os.path.join(d, "state.json"), "w") as fh:
-                            json.dump(state, fh, indent=2, sort_keys=True, default=str)
+                            json.dump(st, fh, indent=2, sort_keys=True, default=str)
             for path, obj in (extra_files or {}).items():
                 os.makedirs(os.path.dirname(path), exist_ok=True)
                 torch.save(obj, path + ".tmp")

@@ -40,6 +40,11 @@ class FLConfig:
     global_eval_batch: int = 256        # rows per global-eval forward (accuracy and per-example
                                         # loss do not depend on it; local eval keeps batch_size
                                         # for the reference's sum-of-batch-means loss quirk)
+    global_eval_models: str = "all"     # serverless: "all" = every client model is scored on a
+                                        # disjoint 1/num_clients stride of the global draw (the
+                                        # federation's accuracy; total eval work independent of the
+                                        # GPU count); "client0" = each rank's first client scores
+                                        # the whole draw
     dirichlet_alpha: float = 0.5
     resample_each_round: bool = False   # reference IID scripts draw a fresh random sample every round
     synthetic_signal: Optional[float] = None  # planted class tokens per 64 (None = generator default)
@@ -138,7 +143,8 @@ class FLConfig:
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
-                   "fedavg_weighting": ("examples", "batches", "uniform")}
+                   "fedavg_weighting": ("examples", "batches", "uniform"),
+                   "global_eval_models": ("all", "client0")}
         for k, allowed in choices.items():
             if getattr(self, k) not in allowed:
                 raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")

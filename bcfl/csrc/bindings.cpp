@@ -627,6 +627,46 @@ Tensor linear_dgrad(Tensor g, Tensor w, optional<Tensor> pre, int64_t act) {
   return out;
 }
 
+// into[M, K] += g[M, N] w[N, K] (the residual-branch gradient accumulated by the consumer GEMM's
+// epilogue, ops.ResidualTap); into may be a strided row view
+void linear_dgrad_acc(Tensor g, Tensor w, Tensor into) {
+  check_gemm_operand(g, "g");
+  check_gemm_operand(w, "w");
+  check_gemm_operand(into, "into");
+  TORCH_CHECK(g.size(1) == w.size(0) && into.size(0) == g.size(0) && into.size(1) == w.size(1),
+              "linear_dgrad_acc: g [M,N], w [N,K], into [M,K]");
+  const int M = g.size(0), N = w.size(0), K = w.size(1);
+  bcfl::LinearParams p{g.data_ptr(), w.data_ptr(), into.data_ptr(), g.stride(0), w.stride(0),
+                       into.stride(0), M, K, N};
+  p.epi = bcfl::EPI_ACCUM;
+  check_rc(bcfl::launch_linear_nn(p, stream()), "linear_dgrad_acc");
+}
+
+// y[M, N] += x[M, K] w[N, K]^T (frozen base projection accumulated onto a LoRA delta)
+void linear_fwd_acc(Tensor x, Tensor w, Tensor into) {
+  check_gemm_operand(x, "x");
+  check_gemm_operand(w, "w");
+  check_gemm_operand(into, "into");
+  TORCH_CHECK(x.size(1) == w.size(1) && into.size(0) == x.size(0) && into.size(1) == w.size(0),
+              "linear_fwd_acc: x [M,K], w [N,K], into [M,N]");
+  const int M = x.size(0), N = w.size(0), K = x.size(1);
+  bcfl::LinearParams p{x.data_ptr(), w.data_ptr(), into.data_ptr(), x.stride(0), w.stride(0),
+                       into.stride(0), M, N, K};
+  p.epi = bcfl::EPI_ACCUM;
+  check_rc(bcfl::launch_linear_nt(p, stream()), "linear_fwd_acc");
+}
+
+// whether linear_fwd / linear_dgrad(_acc) take a shape (M rows, N outputs, K reduction)
+bool gemm_native_ok(int64_t M, int64_t N, int64_t K, bool nn, bool accum) {
+  bcfl::G8Params g{nullptr, nullptr, nullptr, 8, 8, 8, (int)M, (int)N, (int)K};
+  g.b_col = nn;
+  g.kc = (int)K;
+  g.bm = bcfl::g8_auto_bm((int)M, (int)N, 1);
+  if (bcfl::g8_supported(g) == 0) return true;
+  if (accum) return false;
+  return N % 128 == 0 && K % 64 == 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
 std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
@@ -661,6 +701,66 @@ Tensor wgrad(Tensor g, Tensor x) { return wgrad_impl(g, x, false)[0]; }
 // (dW, db) with db = colsum(g) fused into the weight-gradient kernel
 std::vector<Tensor> wgrad_bias(Tensor g, Tensor x) { return wgrad_impl(g, x, true); }
 
+// ------------------------------------------------------------------------------------------------
+// g8 (gemm8.hip): out[M, N] (+)= sum_k A(m, k) B(k, n) with a fused epilogue.
+//   a_col = 0: A is [M, K] (row stride lda)   a_col = 1: A is [K, M]
+//   b_col = 0: B is [N, K]                     b_col = 1: B is [K, N]
+//   epi: 0 store, 1 +bias, 2 bias+act (returns {act(pre), pre}), 3 * act'(aux), 4 accumulate into
+//   `out` (must be given), 5 fp32 split-K partials (returns [splits, M, N] fp32)
+std::vector<Tensor> gemm8(Tensor A, Tensor B, bool a_col, bool b_col, int64_t epi, int64_t act,
+                          optional<Tensor> bias, optional<Tensor> aux, optional<Tensor> out,
+                          int64_t bm, int64_t splits, int64_t kc) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && A.dim() == 2 && B.dim() == 2, "gemm8: 2-D GPU operands");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm8: bf16");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm8: contiguous rows");
+  const int64_t M = a_col ? A.size(1) : A.size(0);
+  const int64_t K = a_col ? A.size(0) : A.size(1);
+  const int64_t N = b_col ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_col ? B.size(0) : B.size(1)) == K, "gemm8: reduction dims differ");
+  bcfl::G8Params p{A.data_ptr(), B.data_ptr(), nullptr, A.stride(0), B.stride(0), N, (int)M,
+                   (int)N, (int)K};
+  p.a_col = a_col;
+  p.b_col = b_col;
+  p.bm = (int)bm;  // 0 = auto
+  p.epi = (int)epi;
+  p.act = (int)act;
+  p.splits = (int)std::max<int64_t>(1, splits);
+  p.kc = kc > 0 ? (int)kc : (int)K;
+  Tensor o, pre, part;
+  if (epi == bcfl::EPI_PARTIAL) {
+    part = torch::empty({p.splits, M, N}, A.options().dtype(torch::kFloat));
+    p.part = part.data_ptr<float>();
+  } else if (out.has_value() && out->defined()) {
+    o = *out;
+    TORCH_CHECK(o.scalar_type() == at::kBFloat16 && o.dim() == 2 && o.size(0) == M &&
+                o.size(1) == N && o.stride(1) == 1, "gemm8: out [M, N] bf16");
+    p.ldc = o.stride(0);
+  } else {
+    TORCH_CHECK(epi != bcfl::EPI_ACCUM, "gemm8: accumulate needs `out`");
+    o = torch::empty({M, N}, A.options());
+  }
+  if (o.defined()) p.C = o.data_ptr();
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous(),
+                "gemm8: bias [N] bf16");
+    p.bias = bias->data_ptr();
+  }
+  if (epi == bcfl::EPI_BIAS_ACT) {
+    pre = torch::empty({M, N}, A.options());
+    p.aux = pre.data_ptr();
+    p.ldaux = N;
+  } else if (epi == bcfl::EPI_DACT) {
+    TORCH_CHECK(aux.has_value() && aux->defined() && aux->size(0) == M && aux->size(1) == N &&
+                aux->stride(1) == 1 && aux->scalar_type() == at::kBFloat16, "gemm8: aux [M, N] bf16");
+    p.aux = aux->data_ptr();
+    p.ldaux = aux->stride(0);
+  }
+  check_rc(bcfl::launch_g8(p, stream()), "gemm8");
+  if (epi == bcfl::EPI_PARTIAL) return {part};
+  if (epi == bcfl::EPI_BIAS_ACT) return {o, pre};
+  return {o};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "bcfl gfx950 (CDNA4) kernels";
   m.def("bdaln_fwd", &bdaln_fwd);
@@ -676,6 +776,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("subset_attn_bwd", &subset_attn_bwd);
   m.def("linear_dgrad", &linear_dgrad);
   m.def("wgrad_bias", &wgrad_bias);
+  m.def("gemm8", &gemm8);
+  m.def("linear_dgrad_acc", &linear_dgrad_acc);
+  m.def("linear_fwd_acc", &linear_fwd_acc);
+  m.def("gemm_native_ok", &gemm_native_ok);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);

@@ -1,0 +1,534 @@
+// g8: the dense-layer GEMMs of every BERT / ALBERT / DistilBERT / Llama projection on MFMA with an
+// 8-phase, LDS-DMA (buffer_load ... lds) software pipeline (SURVEY.md §2.6 K3 / K5 / K6 / K7 and
+// the K9 weight gradient; reference hot path: the HF BertSelfAttention / BertSelfOutput /
+// BertIntermediate / BertOutput dense layers printed at
+// src/Serverlesscase/serverless_cancer_classification_with_BioBERT.ipynb:526-569).
+//
+//   C[M, N] = sum_k A(m, k) B(k, n)     (+ fused epilogue)
+//
+// Operand storage (the "kind" of each operand, compile-time):
+//   A ROW: A(m, k) = A[m * lda + k]  (activations x / dY)    A COL: A(m, k) = A[k * lda + m]  (G^T)
+//   B ROW: B(k, n) = B[n * ldb + k]  (nn.Linear weight, fwd) B COL: B(k, n) = B[k * ldb + n]  (W in
+//                                                              dgrad, X in the weight gradient)
+// so forward = (ROW, ROW), input gradient = (ROW, COL), weight gradient = (COL, COL).
+//
+// Block tile BM x 256 (BM = 256 or 128), 64-deep K-tiles, 8 waves (2 M x 4 N). Each K-tile is
+// staged as four half-tiles (A rows [0, BM/2) / [BM/2, BM), B cols [0, 128) / [128, 256)) in two
+// LDS buffers (even / odd K-tile). A wave owns rows {a BM/2 + wr BM/4 + [0, BM/4)} and columns
+// {b 128 + wc 32 + [0, 32)} for a, b in {0, 1}, i.e. one quadrant (a, b) per half-tile pair, so a
+// K-tile is consumed in 4 phases:
+//     phase 1: ds_read B_lo -> B0, A_lo -> A   MFMA quadrant (0, 0)
+//     phase 2: ds_read B_hi -> B1              MFMA quadrant (0, 1)
+//     phase 3: ds_read A_hi -> A               MFMA quadrant (1, 1)
+//     phase 4: (registers only)                MFMA quadrant (1, 0)
+// Each half-tile of a buffer is last read in a known phase (B_lo 1, A_lo 1, B_hi 2, A_hi 3), so it
+// is re-staged with the K-tile two ahead as soon as the reads are retired: B_lo in phase 2 (its
+// reads are retired by the lgkmcnt before phase 1's barrier), A_lo in 3, B_hi in 4, A_hi in the
+// next tile's phase 1. One LDS-DMA half-tile is issued per phase and three stay in flight across
+// barriers: the only vmcnt waits are the counted ones in phases 4 / 8 (never vmcnt(0) in the main
+// loop) and the barriers are raw s_barrier (a __syncthreads() would drain the DMA queue).
+// The two wave rows run staggered by one barrier (ping-pong): one group's MFMA cluster overlaps
+// the other group's LDS reads and DMA issue. cdna_hip_programming.md §5 "The 256² 8-phase
+// template" (rules T2-T5), re-derived here for three operand layouts.
+//
+// LDS images (one __shared__ array, 128 KiB at BM = 256), written lane-linearly by the DMA; the
+// bank-conflict swizzles are applied on the per-lane SOURCE address and on the read address:
+//   ROW half-tile [H rows][64 k], 128-B rows:  16-B chunk c of row r at chunk c ^ ((r >> 1) & 7)
+//     -> the v_mfma_f32_16x16x32_bf16 operand read (lane: row l & 15, chunk 4s + (l >> 4),
+//        ds_read_b128) hits 16 distinct bank slots in each of its four 16-lane groups;
+//   COL half-tile [64 k][128 idx], 256-B rows: chunk c of k-row r at c ^ ((r & 3) << 2 | (r >> 2) & 3)
+//     -> the operand is read with two ds_read_b64_tr_b16 hardware transposes (k = 8G..8G+3,
+//        8G+4..8G+7 of lane group G), conflict-free per 32-lane half.
+// Epilogues (EPI_*) are applied while the 256 x BN tile streams out through a per-wave LDS slab
+// (16-byte row segments): bias, bias + activation (pre-activation saved), activation' (dgrad of
+// the layer after an activation), accumulate into C (beta = 1), or fp32 split-K partials.
+#include "act.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace bcfl {
+namespace {
+
+constexpr int T8 = 512;  // threads per workgroup (8 waves)
+constexpr int BN8 = 256;
+
+typedef __attribute__((ext_vector_type(8))) short g8_s16x8_t;
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t g8_rsrc(const void* base, int64_t byte_off,
+                                                         int64_t nbytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base) + (uint64_t)byte_off;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  int64_t nb = nbytes < 0 ? 0 : nbytes;
+  if (nb > 0x7fffffff) nb = 0x7fffffff;
+  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)nb);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, (int)n, 0x00020000);
+}
+
+// k-row image swizzle of a COL half-tile with 128 columns (16 chunks of 16 B per row)
+__device__ __forceinline__ int colswz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+#define G8_BAR()                                  \
+  do {                                            \
+    __builtin_amdgcn_sched_barrier(0);            \
+    asm volatile("s_barrier" ::: "memory");       \
+    __builtin_amdgcn_sched_barrier(0);            \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgk_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int BM, bool ACOL, bool BCOL, int EPI, int ACT>
+struct G8 {
+  static constexpr int HA = BM / 2, HB = BN8 / 2;   // half-tile extents (rows of A / cols of B)
+  static constexpr int LA = HA / 64, LB = HB / 64;  // LDS-DMA instructions per thread per half-tile
+  static constexpr int QM = HA / 2, QN = HB / 4;    // wave quadrant: QM rows x QN cols
+  static constexpr int TI = QM / 16, TJ = QN / 16;  // 16 x 16 MFMA tiles per quadrant
+  static constexpr int HBYTES_A = HA * 128, HBYTES_B = HB * 128;
+  static constexpr int BUF = 2 * HBYTES_A + 2 * HBYTES_B;  // one K-tile (A + B)
+  static constexpr int LDS = 2 * BUF;
+  static constexpr int VMN = 2 * LB + LA;  // DMA instructions of the 3 half-tiles left in flight
+  // reads per phase: ROW frag = 1 ds_read_b128, COL frag = 2 ds_read_b64_tr_b16
+  static constexpr int RA0 = TI * 2 * (ACOL ? 2 : 1);
+  static constexpr int RA = RA0 < 15 ? RA0 : 15;  // lgkmcnt is a 4-bit field
+  static_assert(HA % 64 == 0 && TI >= 1 && TJ >= 1, "tile geometry");
+  static_assert(!ACOL || HA == 128, "COL A operand needs 128-row half-tiles");
+};
+
+struct G8Lane {
+  int lane, w, wr, wc;
+};
+
+// ---- one operand ----------------------------------------------------------------------------
+// DMA: half-tile h of K-tile kt -> LDS byte base `dst`. ROW: idx = j*512 + tid -> row idx >> 3,
+// LDS chunk idx & 7 holds source chunk (idx & 7) ^ ((row >> 1) & 7). COL (128 idx per k-row):
+// k-row idx >> 4, LDS chunk idx & 15 holds source chunk (idx & 15) ^ colswz(k-row).
+template <bool COL, int H>
+struct G8Op {
+  static constexpr int L = H / 64;
+  __amdgpu_buffer_rsrc_t rs;
+  int voff[2][L];  // per half: per-thread source byte offsets (k-tile 0)
+  int kbytes;      // source bytes per K-tile
+
+  // ROW: base = rows [i0, i0 + n_rows) of a [*, ld] matrix, K range starts at k0 (elements)
+  // COL: base = k-rows [k0, k_end) of a [*, ld] matrix, columns from i0
+  __device__ __forceinline__ void init(const bf16_t* base, int64_t ld, int i0, int n_valid, int k0,
+                                       int k_end, int tid) {
+    if constexpr (!COL) {
+      rs = g8_rsrc(base, ((int64_t)i0 * ld + k0) * 2, (int64_t)n_valid * ld * 2 - (int64_t)k0 * 2);
+      kbytes = 64 * 2;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int idx = j * T8 + tid;
+          const int r = (idx >> 3);
+          const int c = (idx & 7) ^ ((r >> 1) & 7);
+          voff[h][j] = (int)((int64_t)(h * H + r) * ld * 2) + c * 16;
+        }
+    } else {
+      rs = g8_rsrc(base, (int64_t)k0 * ld * 2, (int64_t)(k_end - k0) * ld * 2);
+      kbytes = (int)(64 * ld * 2);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int idx = j * T8 + tid;
+          const int r = idx >> 4;
+          const int c = (idx & 15) ^ colswz(r);
+          voff[h][j] = (int)((int64_t)r * ld * 2) + (i0 + h * H + c * 8) * 2;
+        }
+    }
+  }
+  // issue the DMA of half-tile h of K-tile kt into LDS byte offset dst (wave w's 1-KiB pieces)
+  __device__ __forceinline__ void dma(char* smem, int dst, int h, int kt, int w) const {
+    // the K-tile offset goes into the per-lane offset (VGPR): the range check, which zero-fills
+    // k-rows past the split end, covers it
+    // (device pass only: the host pass cannot type-check the LDS-DMA builtin, and a failed
+    // host-side instantiation silently drops the kernel's launch stub)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int ko = kt * kbytes;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(smem + dst + j * (T8 * 16) + w * 1024), 16,
+          voff[h][j] + ko, 0, 0, 0);
+    }
+#endif
+  }
+};
+
+// read offsets of one operand's MFMA fragments inside a half-tile (bytes)
+//   ROW: frag (16-row block at `base_idx`, k-step s): lane l -> row l & 15, chunk 4s + (l >> 4)
+//   COL: frag (16-idx block u, k-step s): two transposed reads, k-rows 32s + 8G + q (+4)
+struct G8RowRd {
+  int off[2];
+  __device__ __forceinline__ void init(int lane) {
+    const int r = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = r * 128 + (((4 * s + (lane >> 4)) ^ ((r >> 1) & 7)) << 4);
+  }
+  __device__ __forceinline__ bf16x8_t frag(const char* half, int idx0, int s) const {
+    return *reinterpret_cast<const bf16x8_t*>(half + idx0 * 128 + off[s]);
+  }
+};
+
+// The transposed reads are inline asm: the compiler's waitcnt pass cannot tell the
+// ds_read_tr16 builtin apart from the in-flight LDS-DMA writes and would put a vmcnt(0) (a full
+// drain of the DMA pipeline) in front of every one. hipcc does not count asm loads, so every
+// phase waits lgkmcnt(0) itself after its first barrier and then marks the fragments written
+// (g8_fence) before the MFMAs may read them.
+__device__ __forceinline__ s16x4_t g8_tr_read(uint32_t addr) {
+  s16x4_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+template <int NU>  // NU 16-idx blocks per quadrant
+struct G8ColRd {
+  uint32_t off[NU][2];
+  __device__ __forceinline__ void init(int lane, int u0) {
+    const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kr = 8 * G + q + 4 * h;
+        const int chunk = 2 * (u0 + u) + (p >> 1);
+        off[u][h] = kr * 256 + ((chunk ^ colswz(kr)) << 4) + (p & 1) * 8;
+      }
+  }
+  // half: LDS byte address (32-bit) of the half-tile
+  __device__ __forceinline__ bf16x8_t frag(uint32_t half, int u, int s) const {
+    const s16x4_t lo = g8_tr_read(half + s * 32 * 256 + off[u][0]);
+    const s16x4_t hi = g8_tr_read(half + s * 32 * 256 + off[u][1]);
+    const g8_s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void g8_fence(bf16x8_t (&f)[N][2]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(f[i][s]));
+}
+
+template <int BM, bool ACOL, bool BCOL, int EPI, int ACT>
+__global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
+  using C = G8<BM, ACOL, BCOL, EPI, ACT>;
+  constexpr int TI = C::TI, TJ = C::TJ, QM = C::QM, QN = C::QN, HA = C::HA, HB = C::HB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // ---- tile / split assignment (XCD-aware: each XCD walks a contiguous range of tiles) -------
+  const int tilesN = p.N / BN8;
+  const int tilesM = (p.M + BM - 1) / BM;
+  const int ntile = tilesM * tilesN;
+  const int nwg = ntile * p.splits;
+  const int b = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int tile = L / p.splits, split = L - tile * p.splits;
+  const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN8;
+  const int kbeg = split * p.kc;
+  const int kend = min(p.K, kbeg + p.kc);
+  const int nt = ((kend - kbeg + 127) / 128) * 2;  // K-tiles, even
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- operands ---------------------------------------------------------------------------
+  G8Op<ACOL, HA> opA;
+  G8Op<BCOL, HB> opB;
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* B = reinterpret_cast<const bf16_t*>(p.B);
+  if constexpr (!ACOL) opA.init(A, p.lda, m0, min(BM, p.M - m0), kbeg, kend, tid);
+  else opA.init(A, p.lda, m0, 0, kbeg, kend, tid);
+  if constexpr (!BCOL) opB.init(B, p.ldb, n0, min(BN8, p.N - n0), kbeg, kend, tid);
+  else opB.init(B, p.ldb, n0, 0, kbeg, kend, tid);
+
+  // LDS byte offsets: buffer q, A half a / B half b
+  auto a_half = [&](int q, int a) { return q * C::BUF + a * C::HBYTES_A; };
+  auto b_half = [&](int q, int bh) { return q * C::BUF + 2 * C::HBYTES_A + bh * C::HBYTES_B; };
+
+  const uint32_t lds32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // read-side lane offsets
+  G8RowRd rowrd;
+  rowrd.init(lane);
+  G8ColRd<TI> colA;
+  G8ColRd<TJ> colB;
+  if constexpr (ACOL) colA.init(lane, wr * QM / 16);
+  if constexpr (BCOL) colB.init(lane, wc * QN / 16);
+
+  f32x4_t acc[2][2][TI][TJ];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[a][bb][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fa[TI][2], fb0[TJ][2], fb1[TJ][2];
+
+  auto readA = [&](int q, int a) {
+    const char* hp = smem + a_half(q, a);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (!ACOL) fa[i][s] = rowrd.frag(hp, wr * QM + 16 * i, s);
+        else fa[i][s] = colA.frag(lds32 + a_half(q, a), i, s);
+      }
+  };
+  auto readB = [&](int q, int bh, bf16x8_t (&fb)[TJ][2]) {
+    const char* hp = smem + b_half(q, bh);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (!BCOL) fb[j][s] = rowrd.frag(hp, wc * QN + 16 * j, s);
+        else fb[j][s] = colB.frag(lds32 + b_half(q, bh), j, s);
+      }
+  };
+  auto mma = [&](int a, int bh, const bf16x8_t (&fb)[TJ][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[a][bh][i][j] = mfma16(fa[i][s], fb[j][s], acc[a][bh][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // after a phase's first barrier: its LDS reads have landed (asm transposed reads are not
+  // counted by the compiler, so wait explicitly and mark the fragments written)
+  auto landed = [&](bf16x8_t (&fb)[TJ][2], bool a_read) {
+    if constexpr (ACOL || BCOL) {
+      lgk_wait<0>();
+      if constexpr (BCOL) g8_fence(fb);
+      if constexpr (ACOL) {
+        if (a_read) g8_fence(fa);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // DMA issue helpers (half-tiles of buffer q with K-tile kt)
+  auto dmaA = [&](int q, int a, int kt) { opA.dma(smem, a_half(q, a), a, kt, w); };
+  auto dmaB = [&](int q, int bh, int kt) { opB.dma(smem, b_half(q, bh), bh, kt, w); };
+
+  // ---- prologue: K-tile 0 (all four half-tiles) + K-tile 1 (B_lo, A_lo, B_hi) ---------------
+  dmaB(0, 0, 0);
+  dmaA(0, 0, 0);
+  dmaB(0, 1, 0);
+  dmaA(0, 1, 0);
+  dmaB(1, 0, 1);
+  dmaA(1, 0, 1);
+  dmaB(1, 1, 1);
+  vm_wait<C::VMN>();  // K-tile 0 landed (this wave's pieces) ...
+  G8_BAR();           // ... and every wave's
+  if (wr == 1) G8_BAR();  // stagger: the second wave row runs one barrier behind
+
+  // one K-tile in buffer Q: 4 phases. `full`: issue the DMAs of the K-tiles two ahead.
+  auto ktile = [&](const int Q, int t, bool full) {
+    // phase 1: B_lo -> fb0, A_lo -> fa; DMA A_hi of the other buffer (K-tile t + 1)
+    readB(Q, 0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(Q, 0);
+    if (Q == 0 || full) dmaA(1 - Q, 1, t + 1);
+    lgk_wait<C::RA>();  // B_lo reads retired before the barrier (B_lo is re-staged in phase 2)
+    G8_BAR();
+    landed(fb0, true);
+    mma(0, 0, fb0);
+    G8_BAR();
+    // phase 2: B_hi -> fb1; DMA B_lo (K-tile t + 2)
+    readB(Q, 1, fb1);
+    if (full) dmaB(Q, 0, t + 2);
+    G8_BAR();
+    landed(fb1, false);
+    mma(0, 1, fb1);
+    G8_BAR();
+    // phase 3: A_hi -> fa; DMA A_lo (t + 2)
+    readA(Q, 1);
+    if (full) dmaA(Q, 0, t + 2);
+    G8_BAR();
+    landed(fb1, true);
+    mma(1, 1, fb1);
+    G8_BAR();
+    // phase 4: DMA B_hi (t + 2); retire everything but the last three half-tiles
+    if (full) {
+      dmaB(Q, 1, t + 2);
+      vm_wait<C::VMN>();
+    } else {
+      vm_wait<0>();
+    }
+    G8_BAR();
+    mma(1, 0, fb0);
+    G8_BAR();
+  };
+
+  const int iters = nt >> 1;
+  for (int it = 0; it < iters - 1; ++it) {
+    ktile(0, 2 * it, true);
+    ktile(1, 2 * it + 1, true);
+  }
+  // last pair: the even tile's phase 1 still issues the odd tile's A_hi; no further DMA
+  ktile(0, nt - 2, false);
+  ktile(1, nt - 1, false);
+  if (wr == 0) G8_BAR();  // close the stagger
+  lgk_wait<0>();
+  __syncthreads();
+
+  // ---- epilogue: per-wave LDS slab, 16-byte row segments ------------------------------------
+  constexpr int LDF = QN + 4;  // slab row stride (floats)
+  float* slab = reinterpret_cast<float*>(smem) + w * (QM * LDF);
+  constexpr int LPR = QN / 8;           // lanes per slab row
+  constexpr int RPP = 64 / LPR;         // rows per pass
+  const int rr0 = lane / LPR, cc = (lane % LPR) * 8;
+  bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C);
+  bf16_t* aux = reinterpret_cast<bf16_t*>(p.aux);
+  const bf16_t* bias = reinterpret_cast<const bf16_t*>(p.bias);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bh = 0; bh < 2; ++bh) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            slab[(16 * i + (lane >> 4) * 4 + r) * LDF + 16 * j + (lane & 15)] = acc[a][bh][i][j][r];
+      const int n = n0 + bh * HB + wc * QN + cc;
+      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ACT) {
+        if (bias) Vec8<bf16_t>::load(bias + n, bv);
+      }
+#pragma unroll
+      for (int ps = 0; ps < QM / RPP; ++ps) {
+        const int rr = rr0 + ps * RPP;
+        const int m = m0 + a * HA + wr * QM + rr;
+        float v[8];
+        Vec8<float>::load(slab + rr * LDF + cc, v);
+        if (m < p.M) {
+          if constexpr (EPI == EPI_PARTIAL) {
+            float* dst = p.part + ((int64_t)split * p.M + m) * p.ldc + n;
+            Vec8<float>::store(dst, v);
+          } else {
+            if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += bv[e];
+            } else if constexpr (EPI == EPI_BIAS_ACT) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] + bv[e]));  // pre, as stored
+              Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + n, v);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = act_ft<ACT>(v[e]);
+            } else if constexpr (EPI == EPI_DACT) {
+              float av[8];
+              Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, av);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] *= act_dt<ACT>(av[e]);
+            } else if constexpr (EPI == EPI_ACCUM) {
+              float ov[8];
+              Vec8<bf16_t>::load(Cp + (int64_t)m * p.ldc + n, ov);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += ov[e];
+            }
+            Vec8<bf16_t>::store(Cp + (int64_t)m * p.ldc + n, v);
+          }
+        }
+      }
+    }
+}
+
+template <int BM, bool ACOL, bool BCOL>
+int g8_dispatch(const G8Params& p, hipStream_t s) {
+  const int ntile = ((p.M + BM - 1) / BM) * (p.N / BN8);
+  const dim3 grid(ntile * p.splits), block(T8);
+  constexpr size_t lds = G8<BM, ACOL, BCOL, 0, 0>::LDS;
+#define G8_L(E, A) hipLaunchKernelGGL((g8_kernel<BM, ACOL, BCOL, E, A>), grid, block, lds, s, p)
+  switch (p.epi) {
+    case EPI_STORE: G8_L(EPI_STORE, 0); break;
+    case EPI_BIAS: G8_L(EPI_BIAS, 0); break;
+    case EPI_ACCUM: G8_L(EPI_ACCUM, 0); break;
+    case EPI_PARTIAL: G8_L(EPI_PARTIAL, 0); break;
+    case EPI_BIAS_ACT:
+    case EPI_DACT: {
+      const bool fwd = p.epi == EPI_BIAS_ACT;
+      switch (p.act) {
+        case ACT_GELU: if (fwd) G8_L(EPI_BIAS_ACT, ACT_GELU); else G8_L(EPI_DACT, ACT_GELU); break;
+        case ACT_GELU_TANH:
+          if (fwd) G8_L(EPI_BIAS_ACT, ACT_GELU_TANH); else G8_L(EPI_DACT, ACT_GELU_TANH);
+          break;
+        case ACT_RELU: if (fwd) G8_L(EPI_BIAS_ACT, ACT_RELU); else G8_L(EPI_DACT, ACT_RELU); break;
+        default: return -5;
+      }
+      break;
+    }
+    default: return -4;
+  }
+#undef G8_L
+  return 0;
+}
+
+}  // namespace
+
+// Block-row choice: a launch takes ceil(tiles / 256 CUs) waves of tiles, a 128-row tile takes
+// ~0.57 of a 256-row tile's time (measured 1.15x less efficient per FLOP). Pick the smaller
+// predicted time: on the BERT shapes M = 7680 with N = 768 / 2304 this is 128 (90 -> 180 tiles,
+// 270 -> 540), at M = 11264 and on 4096^3 it is 256 (profiles/g8_v1_vs_hipblaslt.json).
+int g8_auto_bm(int M, int N, int splits) {
+  const int64_t t256 = (int64_t)((M + 255) / 256) * (N / BN8) * splits;
+  const int64_t t128 = (int64_t)((M + 127) / 128) * (N / BN8) * splits;
+  const double c256 = (double)((t256 + 255) / 256) * 256.0;
+  const double c128 = (double)((t128 + 255) / 256) * 128.0 * 1.15;
+  return c128 < c256 ? 128 : 256;
+}
+
+int g8_supported(const G8Params& p) {
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0) return -1;
+  if (p.N % BN8) return -1;
+  if (p.bm != 128 && p.bm != 256 && p.bm > 0) return -1;
+  if (p.a_col && p.bm != 256) return -1;
+  // ROW operands read whole 128-deep K pairs: every split must cover a multiple of 128
+  if ((!p.a_col || !p.b_col) && (p.K % 128 || p.kc % 128)) return -2;
+  if (p.splits < 1 || p.kc <= 0 || (int64_t)p.kc * (p.splits - 1) >= p.K) return -3;
+  if (p.lda % 8 || p.ldb % 8 || p.ldc % 8) return -2;
+  if ((p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) && (!p.aux || p.ldaux % 8)) return -3;
+  if (p.epi == EPI_PARTIAL && !p.part) return -3;
+  return 0;
+}
+
+int launch_g8(const G8Params& p_in, hipStream_t s) {
+  G8Params p = p_in;
+  if (p.bm <= 0) p.bm = p.a_col ? 256 : g8_auto_bm(p.M, p.N, p.splits);
+  const int rc = g8_supported(p);
+  if (rc) return rc;
+  if (p.bm == 256) {
+    if (!p.a_col && !p.b_col) return g8_dispatch<256, false, false>(p, s);
+    if (!p.a_col && p.b_col) return g8_dispatch<256, false, true>(p, s);
+    if (p.a_col && p.b_col) return g8_dispatch<256, true, true>(p, s);
+    return g8_dispatch<256, true, false>(p, s);
+  }
+  if (!p.a_col && !p.b_col) return g8_dispatch<128, false, false>(p, s);
+  if (!p.a_col && p.b_col) return g8_dispatch<128, false, true>(p, s);
+  return -1;
+}
+
+}  // namespace bcfl

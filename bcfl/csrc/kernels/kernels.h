@@ -99,7 +99,8 @@ int wgrad_splits(int M, int N, int K, int* Mc);
 int launch_wgrad(const WgradParams& p, hipStream_t s);
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
-enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3 };
+enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3, EPI_ACCUM = 4,
+                 EPI_PARTIAL = 5 };
 struct LinearParams {
   const void* A;       // [M, K] bf16, row stride lda
   const void* B;       // NT: [N, K] (ldb);  NN: [K, N] (ldb)
@@ -115,6 +116,31 @@ struct LinearParams {
 };
 int launch_linear_nt(const LinearParams& p, hipStream_t s);  // C = A B^T
 int launch_linear_nn(const LinearParams& p, hipStream_t s);  // C = A B
+
+// ---- gemm8.hip: 8-phase LDS-DMA MFMA GEMM (fwd / dgrad / wgrad layouts) --------------------
+// C[M, N] = sum_k A(m, k) B(k, n). a_col: A(m, k) = A[k * lda + m] (else A[m * lda + k]);
+// b_col: B(k, n) = B[k * ldb + n] (else B[n * ldb + k]). Split-K: `splits` slices of `kc` reduction
+// elements each (EPI_PARTIAL writes fp32 part[split][M][ldc]).
+struct G8Params {
+  const void* A;
+  const void* B;
+  void* C;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int a_col = 0, b_col = 0;
+  int bm = 0;                    // block rows: 256 or 128 (block cols are always 256); 0 = auto
+  int epi = EPI_STORE;
+  int act = 0;
+  const void* bias = nullptr;    // [N] bf16
+  void* aux = nullptr;           // [M, N] bf16 (EPI_BIAS_ACT writes, EPI_DACT reads)
+  int64_t ldaux = 0;
+  float* part = nullptr;         // EPI_PARTIAL: fp32 [splits, M, ldc]
+  int splits = 1;
+  int kc = 0;                    // reduction elements per split (multiple of 128 for ROW operands)
+};
+int g8_supported(const G8Params& p);  // 0 = launchable
+int g8_auto_bm(int M, int N, int splits);
+int launch_g8(const G8Params& p, hipStream_t s);
 
 // ---- attention.hip -----------------------------------------------------------------------------
 struct AttnParams {

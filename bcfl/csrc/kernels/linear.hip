@@ -582,8 +582,34 @@ int launch_persist(const LinearParams& p, hipStream_t s) {
   return 0;
 }
 
+// The 8-phase LDS-DMA kernel (gemm8.hip) takes every shape it supports (N % 256, K % 128): it
+// matches or beats hipBLASLt on the BERT projections (profiles/g8_v1_vs_hipblaslt.json); the
+// register-staged kernels below remain for the other shapes. BCFL_G8=0 disables it.
+template <bool NN>
+int try_g8(const LinearParams& p, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("BCFL_G8");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || p.tile >= 0) return 1;
+  G8Params g{p.A, p.B, p.C, p.lda, p.ldb, p.ldc, p.M, p.N, p.K};
+  g.b_col = NN ? 1 : 0;
+  g.epi = p.epi;
+  g.act = p.act;
+  g.bias = p.bias;
+  g.aux = p.aux;
+  g.ldaux = p.ldaux;
+  g.kc = p.K;
+  g.bm = g8_auto_bm(p.M, p.N, 1);
+  if (g8_supported(g) != 0) return 1;
+  return launch_g8(g, s);
+}
+
 template <bool NN>
 int launch_linear_t(const LinearParams& p, hipStream_t s) {
+  if (p.M == 0 && p.N % 128 == 0) return 0;
+  if (p.M > 0 && try_g8<NN>(p, s) == 0) return 0;
+  if (p.epi == EPI_ACCUM) return -4;
   if (p.N % 128 || p.K % LK || p.M < 0 || p.K <= 0) return -1;
   if (p.lda % 8 || p.ldb % 8 || p.ldc % 8 || p.ldaux % 8) return -2;
   if ((p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) && (!p.aux || p.ldaux <= 0)) return -3;

@@ -230,6 +230,9 @@ class Federation:
         self.ckpt = AsyncCheckpointer(self.model, self.flat, cfg.async_ckpt) if (
             cfg.save_every > 0 and (self.rt.is_main or cfg.save_clients)) else None
         self.timer = PhaseTimer(sync_device=cfg.profile)
+        self.timer.on_resolve = lambda rec: self.metrics.write(
+            {"round": rec.get("round"), "device_phases": True,
+             **{k: v for k, v in rec.items() if k.startswith("dev_t_")}})
         self._build_eval_overlap(vocab, mdtype)
         self.global_accuracies: List[float] = []
         self.history: List[dict] = []
@@ -392,9 +395,10 @@ class Federation:
                         next(g)
                     except StopIteration:
                         gens.remove(g)
-        for ln in self.lanes:
-            if ln.stream is not None:
-                main.wait_stream(ln.stream)
+            # the join is part of the phase: its device end event then covers every lane
+            for ln in self.lanes:
+                if ln.stream is not None:
+                    main.wait_stream(ln.stream)
         return out
 
     # ================================ helpers ==================================================
@@ -493,21 +497,82 @@ class Federation:
                                    r if c.resample_each_round else None,
                                    self.test_ds.labels if c.global_test_stratified else None)
 
-    def global_majority_rate(self, r: int) -> float:
-        """Best constant-predictor accuracy on round r's global draw (printed beside accuracy so
-        a collapsed model cannot pass for a trained one)."""
-        return majority_rate(self.test_ds.labels, self.global_test_idx(r))
+    def _sharded_eval(self) -> bool:
+        c = self.cfg
+        return c.mode == "serverless" and c.global_eval_models == "all" and not c.compat_chain
 
-    def global_test_batches(self, r: int):
+    def _global_eval_rows(self, r: int, c: Optional[int] = None) -> np.ndarray:
+        """Rows of round r's global draw scored by client c's model (sharded evaluation: client c
+        takes rows c, c + K, c + 2K, ... of the class-balanced draw) or by this rank (c None:
+        the whole draw when collective-free, else a rank stride of it)."""
         idx = self.global_test_idx(r)
-        # collective-free: every rank scores its own model on the whole draw (no all-reduce)
-        mine = idx if self.collective_free else idx[self.rt.rank::self.rt.world]
+        if c is not None:
+            return idx[c::self.cfg.num_clients]
+        return idx if self.collective_free else idx[self.rt.rank::self.rt.world]
+
+    def global_majority_rate(self, r: int) -> float:
+        """Best constant-predictor accuracy on the rows this rank scored in round r (printed
+        beside accuracy so a collapsed model cannot pass for a trained one)."""
+        if self._sharded_eval():
+            idx = np.concatenate([self._global_eval_rows(r, c) for c in self.local_clients])
+        else:
+            idx = self.global_test_idx(r)
+        return majority_rate(self.test_ds.labels, idx)
+
+    def global_test_batches(self, r: int, c: Optional[int] = None):
+        mine = self._global_eval_rows(r, c)
         if len(mine) == 0:
             return []
         return self._cached_batches(
-            ("global", self._draw_key(r)),
+            ("global", self._draw_key(r), c),
             lambda: ClientLoader(self.test_ds, mine, max(self.cfg.global_eval_batch, 1),
                                  pad_multiple=self.pad_multiple).device_batches(self.device))
+
+    def _global_eval_sets(self, r: int):
+        """[(client, batches)] this rank scores for round r's global evaluation. Sharded
+        (serverless default): every hosted client's mixed model on its stride of the draw, so the
+        federation's models are all scored and the job evaluates the draw exactly once per round
+        whatever the GPU count. Otherwise one model (client None = the model bound to
+        ``self.flat``: the global model in server mode, the first hosted client in serverless)."""
+        if self._sharded_eval():
+            return [(c, self.global_test_batches(r, c)) for c in self.local_clients]
+        return [(None, self.global_test_batches(r))]
+
+    def _bind_client(self, c: Optional[int]) -> None:
+        """Point ``self.flat`` (lane 0's replica) at client c's current state for evaluation."""
+        if c is None or not self.multi:
+            return
+        if self.lanes:
+            self.flat.rebind(self.client_master[c], self.client_param[c])
+        else:
+            self.flat.load_master(self.client_master[c])
+
+    def _client_param(self, c: Optional[int]) -> torch.Tensor:
+        if c is not None and self.lanes:
+            return self.client_param[c]
+        if c is not None and self.multi:
+            raise RuntimeError("overlapped evaluation of a non-resident client")
+        return self.flat.param
+
+    def _note_global_counts(self, r: int, acc4) -> None:
+        self._last_global_counts = (r, float(acc4[0]), float(acc4[1]))
+
+    def federation_accuracy(self) -> Dict[str, float]:
+        """Accuracy of the LAST evaluated round over the whole job (a collective in a
+        collective-free run: every rank's [correct, rows] are gathered). With sharded evaluation
+        this is the mean accuracy of all client models, each on its disjoint stride of the
+        class-balanced draw."""
+        last = getattr(self, "_last_global_counts", None)
+        parts = [last] if not (self.collective_free and self.rt.distributed) else \
+            D.all_gather_object(last)
+        parts = [x for x in parts if x is not None]
+        if not parts:
+            return {}
+        rounds = {x[0] for x in parts}
+        correct = sum(x[1] for x in parts)
+        rows = sum(x[2] for x in parts)
+        return {"accuracy": correct / max(rows, 1.0), "rows": rows, "round": max(rounds),
+                "ranks": len(parts), "rounds_agree": len(rounds) == 1}
 
     def _activate(self, c: int, master: Optional[torch.Tensor] = None):
         if master is not None:
@@ -632,36 +697,54 @@ class Federation:
         self.eval_stream = torch.cuda.Stream(device=self.device)
 
     def _launch_eval_global(self, r: int) -> None:
-        """Snapshot the model the inline path would score and queue its evaluation."""
+        """Snapshot the model(s) the inline path would score and queue their evaluation."""
         self._resolve_eval()
         with self.timer.phase("eval_global"):
-            gb = self.global_test_batches(r)  # first use uploads on the current stream
+            sets = self._global_eval_sets(r)   # first use uploads on the current stream
             main = torch.cuda.current_stream(self.device)
             es = self.eval_stream
-            es.wait_stream(main)               # the mixed model and the batches are ready
+            es.wait_stream(main)               # the mixed model(s) and the batches are ready
+            if not hasattr(self, "_eval_snaps"):
+                self._eval_snaps = {}
             with torch.cuda.stream(es):
-                self.eval_flat.param.copy_(self.flat.param)
+                t_beg = torch.cuda.Event(enable_timing=True)
+                t_beg.record(es)
+                snaps = []
+                for c, _ in sets:
+                    if len(sets) == 1:
+                        snap = self.eval_flat.param
+                    else:
+                        snap = self._eval_snaps.get(c)
+                        if snap is None:
+                            snap = self._eval_snaps[c] = torch.empty_like(self.eval_flat.param)
+                    snap.copy_(self._client_param(c))
+                    snaps.append(snap)
                 copied = torch.cuda.Event()
                 copied.record(es)
-                # later writers of the source (next round's optimizer / mixing, issued on main
-                # or on lane streams that wait on main) are ordered after the snapshot copy
+                # later writers of the sources (next round's optimizer / mixing, issued on main
+                # or on lane streams that wait on main) are ordered after the snapshot copies
                 # only; the forward passes overlap them
                 main.wait_event(copied)
-                acc = (self.eval_trainer.evaluate_device(gb) if gb else
-                       torch.zeros(4, dtype=torch.float64, device=self.device))
-            ev = torch.cuda.Event()
-            ev.record(es)
-            self._eval_pending = (r, acc, gb, ev)
+                acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+                for (c, gb), snap in zip(sets, snaps):
+                    if gb:
+                        self.eval_flat.rebind(self.eval_flat.master, snap)
+                        acc += self.eval_trainer.evaluate_device(gb)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(es)
+            self._eval_pending = (r, acc, sets, ev, t_beg)
 
     def _resolve_eval(self) -> None:
         """Host-read a queued global evaluation and file it under its round."""
         p, self._eval_pending = self._eval_pending, None
         if p is None:
             return
-        r, acc, _batches, ev = p
+        r, acc, _sets, ev, t_beg = p
         ev.synchronize()
+        self.timer.add_hidden("eval_global", t_beg.elapsed_time(ev) / 1000.0)
         a = acc.cpu().tolist()
         ge = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+        self._note_global_counts(r, a)
         self.global_accuracies.append(ge.accuracy)
         if self.verbose and self.cfg.reference_prints:
             print(f"Global Model Accuracy: {ge.accuracy * 100:.2f}%", flush=True)
@@ -675,11 +758,15 @@ class Federation:
 
     def _eval_global(self, r: int) -> EvalResult:
         with self.timer.phase("eval_global"):
-            gb = self.global_test_batches(r)
-            acc = self.trainer.evaluate_device(gb) if gb else torch.zeros(4, dtype=torch.float64, device=self.device)
+            acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+            for c, gb in self._global_eval_sets(r):
+                if gb:
+                    self._bind_client(c)
+                    acc += self.trainer.evaluate_device(gb)
             if not self.collective_free:
                 D.all_reduce_(acc)
             a = acc.cpu().tolist()
+        self._note_global_counts(r, a)
         return EvalResult(int(a[0]), int(a[1]), a[2], a[3])
 
     # ================================ rounds ====================================================
@@ -773,10 +860,13 @@ class Federation:
         roots; every verified receive becomes a ``verify`` block (verdict accept / reject)."""
         out = []
         by_client = {x["client"]: x for x in recs}
-        for g in getattr(self.gossip, "records", []):
+        take = getattr(self.gossip, "take_records", None)
+        for g in (take() if take is not None else []):
             if g["kind"] == "update":
                 if g.get("root_t") is not None and g["client"] in by_client and self._gossip_roots:
-                    by_client[g["client"]]["root"] = ops.root_bytes(g["root_t"]).hex()
+                    rt_ = g["root_t"]
+                    by_client[g["client"]]["root"] = rt_ if isinstance(rt_, str) else \
+                        ops.root_bytes(rt_).hex()
                 if g["client"] in by_client:
                     by_client[g["client"]].setdefault("metrics", {})["version"] = g["version"]
             elif g["kind"] == "recv":
@@ -929,6 +1019,7 @@ class Federation:
 
     def run_round(self, r: int) -> dict:
         self._log_provenance(r)
+        self.timer.begin_round()
         t0 = time.perf_counter()
         res = self.server_round(r) if self.cfg.mode == "server" else self.serverless_round(r)
         ge: Optional[EvalResult] = res.get("global")
@@ -946,6 +1037,7 @@ class Federation:
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
                "dead_peers": res.get("dead_peers", []),
+               **{k: res[k] for k in ("mixed", "stale_rounds", "torn", "rejected_msgs") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
         if self.is_cuda:
@@ -953,8 +1045,9 @@ class Federation:
         for c, n_, m in res.get("client_metrics", []):
             self.metrics.write({"round": r, "client": c, "local_acc": m.get("accuracy"),
                                 "local_loss": m.get("loss"), "examples": n_})
-        self.metrics.write(rec)
         self.history.append(rec)
+        self.timer.end_round(rec)  # device phase times land in rec once their events complete
+        self.metrics.write({k: v for k, v in rec.items() if not k.startswith("dev_t_")})
         if self.cfg.progress:
             self.log(f"[round {r}] {t_round:.2f} s  global_acc={gacc}  train_loss={rec['train_loss']}")
         return rec
@@ -967,11 +1060,31 @@ class Federation:
         cfg = self.cfg
         if self.ckpt is None or (r + 1) % cfg.save_every:
             return
+        if self.ckpt.busy():
+            if cfg.save_resume_state:
+                # resumable runs never skip: every rank's files of a save belong to ONE round
+                # (independent skips would let global/, client_*/ and resume/rank*.pt disagree)
+                self.ckpt.wait()
+            else:
+                self.ckpt.skipped += 1   # skip BEFORE building any state (no wasted D2H copies)
+                return
         with self.timer.phase("ckpt"):
+            accs = list(self.global_accuracies)
             state = {"round": r, "rng": ops.rng.global_rng().state(),
                      "ledger_tip": self.ledger.tip if self.ledger else None,
                      "ledger_height": len(self.ledger) if self.ledger else 0,
-                     "global_accuracies": self.global_accuracies, "config": cfg.to_dict()}
+                     "global_accuracies": accs, "config": cfg.to_dict()}
+            pend = self._eval_pending
+            if pend is not None and pend[0] == r:
+                # round r's overlapped evaluation is still running: the writer thread waits for
+                # its event and files the accuracy (no stall of the training stream here)
+                _r, acc_t, _sets, ev_t, _t0 = pend
+
+                def _fin(accs=accs, acc_t=acc_t, ev_t=ev_t):
+                    ev_t.synchronize()
+                    a = acc_t.cpu().tolist()
+                    return {"global_accuracies": accs + [a[0] / max(a[1], 1.0)]}
+                state["_finalize"] = _fin
             jobs = []
             if self.rt.is_main:
                 src = self.global_master if cfg.mode == "server" else self.flat.master
@@ -1001,7 +1114,9 @@ class Federation:
                              for c, o in self.client_opt.items()},
               "prev_rejected": sorted(self.prev_verdicts.rejected),
               "drift": self.drift.state_dict(),
-              "tokens_trained": int(self.tokens_trained)}
+              "tokens_trained": int(self.tokens_trained),
+              "ledger_tip": self.ledger.tip if self.ledger else None,
+              "ledger_height": len(self.ledger) if self.ledger else 0}
         if self.global_master is not None:
             st["global_master"] = cpu(self.global_master)
         if self.gossip is not None and hasattr(self.gossip, "state_dict"):
@@ -1023,6 +1138,7 @@ class Federation:
             self.gossip.drain()
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
+        self.timer.resolve(block=True)
 
     def audit_ledgers(self) -> Dict[str, int]:
         """Cross-rank audit of the per-rank chains of a collective-free federation: every update
@@ -1097,17 +1213,29 @@ class Federation:
         self.start_round = int(st["round"]) + 1
         self.global_accuracies = list(st.get("global_accuracies", []))
         rs = os.path.join(path, "resume", f"rank{self.rt.rank}.pt")
+        rst = None
         if os.path.exists(rs):
-            self._load_resume_state(torch.load(rs, weights_only=True, map_location="cpu"))
-        led = os.path.join(path, "ledger.jsonl")
+            rst = torch.load(rs, weights_only=True, map_location="cpu")
+            if int(rst["round"]) != int(st["round"]):
+                raise RuntimeError(f"resume state {rs} is from round {rst['round']} but "
+                                   f"global/state.json is from round {st['round']}: the "
+                                   "checkpoint files belong to different rounds")
+            self._load_resume_state(rst)
+        # each rank continues ITS OWN chain: collective-free runs keep one chain per rank
+        # (ledger.rank{k}.jsonl), collective runs one canonical chain (ledger.jsonl)
+        mine = self._ledger_path()
+        led = os.path.join(path, os.path.basename(mine) if mine else "ledger.jsonl")
+        tip, height = st.get("ledger_tip"), st.get("ledger_height")
+        if rst is not None and "ledger_tip" in rst:
+            tip, height = rst.get("ledger_tip"), rst.get("ledger_height")
         if self.ledger is not None and os.path.exists(led):
             old = Ledger.load(led)
             if old.verify() != -1:
                 raise RuntimeError("ledger in resume dir fails verification")
-            if st.get("ledger_height") and len(old) > int(st["ledger_height"]):
-                old = old.truncated(int(st["ledger_height"]))  # blocks after the checkpoint
-            if st.get("ledger_tip") and old.tip != st["ledger_tip"]:
-                raise RuntimeError("ledger tip does not match the checkpoint's ledger_tip")
+            if height and len(old) > int(height):
+                old = old.truncated(int(height))  # blocks after the checkpoint
+            if tip and old.tip != tip:
+                raise RuntimeError(f"ledger tip of {led} does not match the checkpoint's ledger_tip")
             self.ledger = old
             self.ledger.path = self._ledger_path()  # continue the chain in this run's out_dir
             self.ledger.rewrite()

@@ -107,13 +107,20 @@ def _wgrad_async(g2, x2, want_b):
     return dw, db
 
 
-# Plain (epilogue-free) forward / input-gradient GEMMs go to hipBLASLt by default: on the bench
-# shapes (K = 768 / 3072, 12-48 reduction steps) it is 1.2-1.4x faster than linear.hip's
-# register-staged tiles in isolation and equal inside the 8-lane bench
-# (profiles/linear_gemm_vs_hipblaslt.md). The fused-epilogue GEMMs (bias+GELU forward, GELU'
-# dgrad) always run on linear.hip — that fusion is what the library cannot do (K6).
-# BCFL_GEMM_PLAIN=1 routes the plain GEMMs to linear.hip as well.
-_GEMM_PLAIN_NATIVE = os.environ.get("BCFL_GEMM_PLAIN", "0") == "1"
+# Forward / input-gradient GEMMs run on bcfl's own MFMA kernels: linear.hip routes every shape
+# it can to the 8-phase LDS-DMA kernel (gemm8.hip), which matches or beats hipBLASLt on all eight
+# BERT-base projection shapes (profiles/g8_v1_vs_hipblaslt.json), and keeps its register-staged
+# tiles for the rest. BCFL_GEMM_PLAIN=0 sends the plain (epilogue-free) GEMMs back to the
+# library (A/B runs); the fused-epilogue GEMMs (bias+GELU forward, GELU' dgrad) always run here.
+_GEMM_PLAIN_NATIVE = os.environ.get("BCFL_GEMM_PLAIN", "1") == "1"
+
+
+def _native_accum_ok(m: int, n: int, k: int, nn_: bool, *ts: torch.Tensor) -> bool:
+    """The accumulate-into-C GEMM (beta = 1 epilogue) takes this shape natively (gemm8.hip)."""
+    if not (_GEMM_PLAIN_NATIVE and all(t.dtype == torch.bfloat16 and t.stride(-1) == 1
+                                       and t.stride(0) % 8 == 0 for t in ts)):
+        return False
+    return bool(native().gemm_native_ok(m, n, k, nn_, True))
 
 
 def gemm_supported(x2: torch.Tensor, w: torch.Tensor, nn_: bool = False, op: str = "gemm") -> bool:
@@ -165,6 +172,10 @@ class ResidualTap:
 def _dgrad_into(g2: torch.Tensor, w: torch.Tensor, tap: Optional[ResidualTap]) -> torch.Tensor:
     if tap is not None and tap.g is not None:
         acc, tap.g = tap.g.view(-1, w.shape[1]), None
+        if use_native(g2) and w.is_contiguous() and _native_accum_ok(
+                g2.shape[0], w.shape[1], w.shape[0], True, g2, w, acc):
+            native().linear_dgrad_acc(g2, w, acc)   # acc += g2 W in the GEMM epilogue
+            return acc
         return acc.addmm_(g2, w)
     return _dgrad_gemm(g2, w)
 
@@ -296,7 +307,13 @@ class _LoRALinear(torch.autograd.Function):
         xa = x2 @ a.t()                                   # [M, n r]
         bbd = torch.block_diag(*bs)                       # [N, n r]
         y = torch.mm(xa * s, bbd.t())                     # scale on the [M, n r] side
-        y.addmm_(x2, w.t())                               # base GEMM accumulates in place
+        if x2.stride(-1) != 1 or x2.stride(0) % 8:
+            x2 = x2.contiguous()
+        if w.is_contiguous() and _native_accum_ok(x2.shape[0], w.shape[0], w.shape[1], False,
+                                                   x2, w, y):
+            native().linear_fwd_acc(x2, w, y)             # base GEMM accumulates in its epilogue
+        else:
+            y.addmm_(x2, w.t())
         ctx.save_for_backward(x2, w, a, xa, bbd)
         ctx.s, ctx.sizes, ctx.xshape = s, sizes, x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -309,7 +326,7 @@ class _LoRALinear(torch.autograd.Function):
         gb = g2 @ bbd                                     # [M, n r]
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = g2 @ w
+            dx = _dgrad_gemm(g2, w) if w.is_contiguous() else g2 @ w
             dx.addmm_(gb, a, alpha=s)                     # LoRA input gradient, in place
             dx = dx.view(ctx.xshape)
         da = (gb.t() @ x2).mul_(s) if ctx.needs_input_grad[2] else None

@@ -230,7 +230,9 @@ class GossipEngine:
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
         """Sync: publish -> exchange -> wait -> mix.  Async: wait(prev) -> mix -> publish -> launch."""
         info = {"mixed": 0.0, "stale_rounds": 0.0}
-        self.records = []
+        # records are NOT cleared here: a finish() run outside a round (state_dict during a
+        # checkpoint) appends verify blocks that must still reach the ledger; the federation
+        # takes them with take_records()
         if not self.async_gossip:
             self.publish(round_idx, steps)
             self.launch(round_idx)
@@ -260,6 +262,11 @@ class GossipEngine:
     def close(self):
         self.drain()
 
+    def take_records(self) -> List[dict]:
+        """Ledger records produced since the last call (published roots + verified receives)."""
+        out, self.records = self.records, []
+        return out
+
     # ------------------------------------------------------------------------------------
     def state_dict(self) -> dict:
         """Everything a resumed run needs to continue bit-identically: wire snapshots / error-
@@ -276,6 +283,7 @@ class GossipEngine:
               "pending_round": -1 if self.pending_round is None else int(self.pending_round)}
         if self.wire == "bf16_delta":
             st["ref"], st["replica"] = t(self.ref), t(self.replica)
+        st["records"] = _portable_records(self.records)
         return st
 
     def load_state_dict(self, st: dict):
@@ -294,6 +302,20 @@ class GossipEngine:
         self.ready = bool(st["ready"])
         self.pending = None
         self.pending_round = None if int(st["pending_round"]) < 0 else int(st["pending_round"])
+        self.records = list(st.get("records", []))
+
+
+def _portable_records(recs: List[dict]) -> List[dict]:
+    """Not-yet-ledgered records in a form ``torch.load(weights_only=True)`` reads back (device
+    roots become hex strings): a checkpoint taken between an exchange and the next ledger round
+    carries them, so a resumed run ledgers exactly the blocks the uninterrupted run does."""
+    out = []
+    for g in recs:
+        g = dict(g)
+        if g.get("root_t") is not None and not isinstance(g["root_t"], str):
+            g["root_t"] = ops.root_bytes(g["root_t"]).hex()
+        out.append(g)
+    return out
 
 
 @torch.no_grad()
@@ -430,10 +452,16 @@ class MailboxGossip:
             t0 = _time.perf_counter()
             need = {j for j in self.remote_needed if j not in self.dead}
             have = {j for j, s in got.items() if s.round >= round_idx}
+            if not hasattr(self, "scratch"):
+                self.scratch = {j: torch.empty_like(self.stage[j]) for j in self.remote_needed}
             while need - have and _time.perf_counter() - t0 < self.sync_timeout_s:
                 _time.sleep(0.0005)
+                # re-fetch into scratch buffers: a torn re-fetch must not overwrite the complete
+                # snapshot already staged for j (got[j] keeps describing stage[j])
                 more = self.transport.fetch({j: max(self.applied[j], got[j].version if j in got else 0)
-                                             for j in need - have}, self.stage)
+                                             for j in need - have}, self.scratch)
+                for j in more:
+                    self.stage[j], self.scratch[j] = self.scratch[j], self.stage[j]
                 got.update(more)
                 have |= {j for j, s in more.items() if s.round >= round_idx}
         self.torn = self.transport.torn
@@ -473,7 +501,6 @@ class MailboxGossip:
     def end_of_round(self, round_idx: int, W: np.ndarray,
                      param_out: Optional[Dict[int, torch.Tensor]] = None,
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
-        self.records = []
         b0 = self.transport.bytes_posted
         self.publish(round_idx, steps)
         self.collect(round_idx)
@@ -491,6 +518,10 @@ class MailboxGossip:
     def close(self):
         self.transport.close()
 
+    def take_records(self) -> List[dict]:
+        out, self.records = self.records, []
+        return out
+
     def state_dict(self) -> dict:
         """Published snapshots, verified replicas, versions and liveness. Inbox contents are NOT
         state: after a restart peers simply post again (a replica's version tells what is new)."""
@@ -499,7 +530,8 @@ class MailboxGossip:
         return {"send_buf": {int(c): [b.detach().cpu().clone() for b in v] for c, v in self.send_buf.items()},
                 "replica": t(self.replica), "version": dict(self.version), "steps": dict(self.steps),
                 "applied": dict(self.applied), "replica_round": dict(self.replica_round),
-                "dead": sorted(self.dead), "rejected_msgs": self.rejected_msgs}
+                "dead": sorted(self.dead), "rejected_msgs": self.rejected_msgs,
+                "records": _portable_records(self.records)}
 
     def load_state_dict(self, st: dict):
         for c, bufs in st["send_buf"].items():
@@ -511,3 +543,4 @@ class MailboxGossip:
             getattr(self, name).update({int(k): int(v) for k, v in st[name].items()})
         self.dead = set(int(x) for x in st["dead"])
         self.rejected_msgs = int(st["rejected_msgs"])
+        self.records = list(st.get("records", []))

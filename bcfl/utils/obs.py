@@ -42,13 +42,46 @@ def _roctx_pop():
 
 
 class PhaseTimer:
-    """Host monotonic timers per phase (optionally synchronising the device at boundaries)."""
+    """Per-phase timers: host monotonic time, and (GPU) device time from HIP events.
 
-    def __init__(self, sync_device: bool = False, roctx: bool = True):
+    Host time ends when a phase has ISSUED its work; with asynchronous launches the device wait
+    then shows up in whichever later phase first reads a result. The device timer records one
+    HIP event on the issuing (main) stream at the end of every phase: phase k's device time is
+    the interval from the previous phase's end event to its own, so the device phases of a round
+    tile its device timeline exactly (an idle gap is charged to the phase that follows it) and
+    sum to the round's device span. Work on side streams that the main stream never waits for
+    (the overlapped global evaluation, mailbox posts) is reported separately as hidden time
+    (``add_hidden``). Events are read back lazily (``resolve``) so timing never stalls a round."""
+
+    def __init__(self, sync_device: bool = False, roctx: bool = True, device_events: bool = True):
         self.sync_device = sync_device and torch.cuda.is_available()
         self.roctx = roctx
+        self.dev = device_events and torch.cuda.is_available()
         self.totals: Dict[str, float] = defaultdict(float)
         self.counts: Dict[str, int] = defaultdict(int)
+        self.hidden: Dict[str, float] = defaultdict(float)
+        self._marks = []          # [(phase, end event)] of the current round
+        self._last = None         # end event of the previous phase (device timeline anchor)
+        self._pending = []        # [(record, start event, marks)] awaiting read-back
+        self.on_resolve = None    # callback(record) once a round's device times are filled in
+
+    def _mark(self, name: str):
+        if not self.dev:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self._marks.append((name, ev))
+        self._last = ev
+
+    def begin_round(self):
+        """Anchor the round's device timeline at the previous phase's end event (first round:
+        an event recorded now), so consecutive rounds tile the device timeline."""
+        if not self.dev:
+            return
+        if self._last is None:
+            self._last = torch.cuda.Event(enable_timing=True)
+            self._last.record()
+        self._start = self._last
 
     @contextlib.contextmanager
     def phase(self, name: str):
@@ -64,15 +97,54 @@ class PhaseTimer:
                 torch.cuda.synchronize()
             self.totals[name] += time.perf_counter() - t0
             self.counts[name] += 1
+            self._mark(name)
             if self.roctx:
                 _roctx_pop()
 
+    def add_hidden(self, name: str, seconds: float):
+        """Device time of side-stream work the main stream does not wait for."""
+        self.hidden[name] += float(seconds)
+
     def snapshot(self, reset: bool = True) -> Dict[str, float]:
         out = {f"t_{k}": v for k, v in self.totals.items()}
+        if self.hidden:
+            out.update({f"t_hidden_{k}": v for k, v in self.hidden.items()})
+            out["t_overlap_hidden"] = sum(self.hidden.values())
         if reset:
             self.totals.clear()
             self.counts.clear()
+            self.hidden.clear()
         return out
+
+    def end_round(self, rec: Dict[str, Any]):
+        """Queue the round's device phases for read-back into ``rec`` (``dev_t_*`` keys)."""
+        if not self.dev:
+            return
+        self._mark("other")  # host work after the last phase (history, metrics)
+        start = getattr(self, "_start", None)
+        if start is not None and self._marks:
+            self._pending.append((rec, start, self._marks))
+        self._marks = []
+        self._start = None
+        self.resolve(block=False)
+
+    def resolve(self, block: bool = False):
+        """Fill ``dev_t_*`` of every queued round whose events have completed (all of them with
+        ``block``; events complete in stream order, so stop at the first pending one)."""
+        while self._pending:
+            rec, start, marks = self._pending[0]
+            if not (block or marks[-1][1].query()):
+                break
+            self._pending.pop(0)
+            dev: Dict[str, float] = defaultdict(float)
+            prev = start
+            for name, ev in marks:
+                dev[name] += prev.elapsed_time(ev) / 1000.0
+                prev = ev
+            rec.update({f"dev_t_{k}": v for k, v in dev.items()})
+            rec["dev_t_round"] = sum(dev.values())
+            if self.on_resolve is not None:
+                self.on_resolve(rec)
 
 
 class MetricsWriter:

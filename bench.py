@@ -4,12 +4,19 @@ gossip, Non-IID — BASELINE.json's metric on BASELINE.json config 3.
 
 One "step" = one federated ROUND of an 8-client federation: every client trains one local epoch
 (240 samples = 8 batches of 32, reference ``serverless_NonIID_IMDB.py:59``), evaluates on its 60
-local test rows, publishes its model over RCCL send/recv (async, overlapped with the next round),
-mixes its neighbours' models, the federation evaluates the global model on a 100-row draw, every
-client update is Merkle-hashed into the ledger, and the global model is checkpointed (async).
+local test rows, publishes its model into its peers' one-sided hipIpc mailboxes (async: the copy
+runs on a side stream while the next round trains; receivers mix the newest complete snapshot),
+every received payload is re-hashed and checked against its sender's committed Merkle root
+before it is mixed (only at N > 1: with all 8 clients on one rank nothing crosses a process),
+every client model is scored on its stride of a class-balanced 1000-row global draw (overlapped
+with the next round on a side stream), every update is chained into the ledger, and the model is
+checkpointed (async).
 
 Scaling: the federation always has 8 clients (the config names 8); N GPUs host 8/N clients each
 (strong scaling over GPUs). ``value`` = seconds per round for the whole job (max over ranks).
+The JSON also carries device-time phases per round (HIP events, min / max over ranks), the
+overlapped (hidden) side-stream time, process-start-to-end latency (the reference's "Latency"),
+and with N > 1 the measured mailbox post bandwidth, staleness and verification counts.
 
     python bench.py                                   # 1 GPU, 8 virtual clients
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
@@ -21,6 +28,8 @@ import json
 import os
 import sys
 import time
+
+T_IMPORT = time.time()
 
 # reference serverless IMDB latency (All_graphs_IMDB_dataset.ipynb:748): 27.8 min @5 workers,
 # 40 min @10 workers over 20 rounds -> 1.39 / 2.00 min/round; linear interpolation at 8 clients:
@@ -56,6 +65,8 @@ def parse():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
     ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
+    ap.add_argument("--global-test-samples", type=int, default=0,
+                    help="override the global evaluation draw (experiments only; 0 = preset)")
     ap.add_argument("--micro-batches", type=int, default=0,
                     help="ranks training one client at a time: 2 = concurrent micro-batches, 1 = off, 0 = auto")
     return ap.parse_args()
@@ -100,7 +111,9 @@ def main():
                      async_gossip=not a.sync, ledger=not a.no_ledger,
                      save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
                      device=a.device, client_lanes=a.lanes, micro_batches=a.micro_batches,
-                     overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad))
+                     overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad),
+                     **({"global_test_samples": a.global_test_samples}
+                        if a.global_test_samples > 0 else {}))
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
         fed.run_round(r)
@@ -120,14 +133,36 @@ def main():
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = D.max_over_ranks(dt)
+    fed.timer.resolve(block=True)
+    fa = fed.federation_accuracy()  # collective in a multi-rank run: every rank calls it
     tokens = float(fed.tokens_trained - tok0)
     tok_t = torch.tensor([tokens], dtype=torch.float64, device=fed.device)
     D.all_reduce_(tok_t)
     tokens = float(tok_t.item())
-    final_acc = fed.global_accuracies[-1] if fed.global_accuracies else None
+    final_acc = fa.get("accuracy") if fa else (fed.global_accuracies[-1] if fed.global_accuracies else None)
     last = fed.history[-1]
     s_per_round = dt / a.steps
     phases = {k: v for k, v in last.items() if k.startswith("t_")}
+    dev_phases = {k: v for k, v in last.items() if k.startswith("dev_t_")}
+    timed = [h for h in fed.history if a.warmup <= h.get("round", -1) < a.warmup + a.steps]
+    dev_mean, host_mean = {}, {}
+    for h in timed:
+        for k, v in h.items():
+            if k.startswith("dev_t_") or k.startswith("t_hidden_") or k == "t_overlap_hidden":
+                dev_mean[k] = dev_mean.get(k, 0.0) + v / max(len(timed), 1)
+            elif k.startswith("t_"):
+                host_mean[k] = host_mean.get(k, 0.0) + v / max(len(timed), 1)
+    # per-rank spread of the timed rounds' mean device phases
+    allr = D.all_gather_object(dev_mean) if rt.distributed else [dev_mean]
+    spread = {k: {"min": min(d.get(k, 0.0) for d in allr), "max": max(d.get(k, 0.0) for d in allr)}
+              for k in sorted(set().union(*allr))}
+    multi = {}
+    if rt.world > 1:
+        ex = {"stale_rounds": [h.get("stale_rounds") for h in timed],
+              "torn": sum(float(h.get("torn") or 0.0) for h in timed),
+              "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
+              "mixed": sum(float(h.get("mixed") or 0.0) for h in timed)}
+        multi = {"per_rank": D.all_gather_object(ex)}
     ck = fed.ckpt
     # measured peer-copy times of the mailbox posts (multi-rank runs: one model update to one
     # peer over xGMI), read before finish() closes the transport
@@ -149,6 +184,14 @@ def main():
             "speedup_vs_baseline": BASELINE_S_PER_ROUND / s_per_round,
             "baseline_s_per_round": BASELINE_S_PER_ROUND,
             "final_accuracy": final_acc,
+            "final_accuracy_scope": (
+                f"mean over all {a.clients} client models, each scored on a disjoint "
+                f"1/{a.clients} stride of the class-balanced {cfg.global_test_samples}-row draw "
+                f"({int(fa.get('rows', 0))} rows, round {fa.get('round')}, gathered from "
+                f"{fa.get('ranks')} rank(s))" if fa and cfg.mode == "serverless" and
+                cfg.global_eval_models == "all" else
+                "the global model on the draw" if cfg.mode == "server" else
+                "each rank's first client model on the draw (rank 0 reported)"),
             "final_majority_rate": last.get("global_majority_rate"),
             "global_eval_rows": last.get("global_eval_rows"),
             "final_train_loss": last.get("train_loss"),
@@ -181,6 +224,17 @@ def main():
                        "audit": fed.ledger_audit,
                        "rejected_msgs": last.get("rejected_msgs")},
             "last_round_phases_s": phases,
+            "last_round_device_phases_s": dev_phases,
+            "timed_rounds_device_phases_mean_s": dev_mean,
+            "timed_rounds_host_phases_mean_s": host_mean,
+            "device_phases_rank_spread_s": spread,
+            "device_span_vs_wall": (dev_mean.get("dev_t_round", 0.0) / s_per_round) if s_per_round else None,
+            "process_latency_s": {"import_to_end": time.time() - T_IMPORT,
+                                  "note": "process start (module import) to the end of the "
+                                          "timed rounds incl. model build, data synthesis and "
+                                          "warm-up — the reference's 'Latency' "
+                                          "(server_IID_IMDB.py:59-63,229-233)"},
+            **({"multi_rank": multi} if multi else {}),
             "hbm_peak_gb": fed.history[-1].get("hbm_peak_gb"),
         }
         print(json.dumps(rec), flush=True)
