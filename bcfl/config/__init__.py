@@ -77,6 +77,11 @@ class FLConfig:
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
     server_wire_dtype: str = "fp32"     # server FedAvg reduction on the wire: fp32 all-reduce |
                                         # bf16 (delta-coded all-to-all + all-gather, fp32 accumulate)
+    server_transport: str = "rccl"      # server FedAvg: rccl (all-reduce, fastest, every rank must
+                                        # be live) | mailbox (one-sided posts of each rank's partial
+                                        # sum; a rank that stops posting is left out and the weights
+                                        # re-normalised over the live ranks — Flower accept_failures)
+    server_timeout_s: float = 120.0     # mailbox server: how long a round waits for a rank's post
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
     micro_batches: int = 0              # a rank training ONE client at a time splits each batch into
@@ -140,6 +145,7 @@ class FLConfig:
                    "topology": ("full", "ring", "pagerank"),
                    "gossip_transport": ("auto", "mailbox", "rccl"),
                    "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
+                   "server_transport": ("rccl", "mailbox"),
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
@@ -148,6 +154,9 @@ class FLConfig:
         for k, allowed in choices.items():
             if getattr(self, k) not in allowed:
                 raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")
+        if self.mode == "server" and self.server_transport == "mailbox" and self.anomaly_filter != "none":
+            raise ValueError("server_transport='mailbox' aggregates without collectives; the update "
+                             "anomaly filter needs the global view (use server_transport='rccl')")
         if self.deterministic and self.async_gossip and self.gossip_transport == "mailbox":
             raise ValueError("deterministic=True needs a fixed gossip schedule: the one-sided "
                              "mailbox mixes whatever snapshot is newest (timing-dependent); use "

@@ -153,7 +153,7 @@ class Federation:
         # lanes train every hosted client IN PLACE on its own resident buffers (FlatParams.rebind):
         # no per-client master copies in / out of a lane replica
         self.client_param: Dict[int, torch.Tensor] = {}
-        if self.lanes:
+        if self.lanes and cfg.mode == "serverless":
             for c in self.local_clients:
                 self.client_param[c] = torch.empty(self.flat.numel, dtype=self.flat.dtype,
                                                    device=self.device)
@@ -181,6 +181,14 @@ class Federation:
         # the others. The update anomaly filter needs a global view and keeps its collectives.
         self.collective_free = (cfg.mode == "serverless" and self.transport == "mailbox"
                                 and cfg.anomaly_filter == "none" and not cfg.compat_chain)
+        # server FedAvg over mailboxes (liveness: a dead rank is left out, weights re-normalised)
+        self.server_mbox = None
+        if cfg.mode == "server" and cfg.server_transport == "mailbox":
+            self.collective_free = True
+            if self.rt.distributed:
+                from ..parallel.fedavg import MailboxFedAvg
+                self.server_mbox = MailboxFedAvg(self.flat.numel, self.device,
+                                                 cfg.server_timeout_s, cfg.verify_updates)
         self.excluded: List[int] = []
         self.gossip: Optional[GossipEngine] = None
         if cfg.mode == "serverless" and not cfg.compat_chain:
@@ -255,10 +263,12 @@ class Federation:
     # ================================ lanes ====================================================
     def _build_lanes(self, vocab: int, mdtype: torch.dtype) -> List[ClientLane]:
         cfg = self.cfg
-        if not (cfg.mode == "serverless" and self.multi and not cfg.compat_chain):
+        if not (self.multi and not cfg.compat_chain):
             return []
         if cfg.deterministic:
             n = 1  # concurrent lanes reorder library reductions (timing-dependent, ~1e-7)
+        elif cfg.micro_batches == 2:
+            n = 1  # concurrency comes from the two micro-batch streams of the one lane
         elif cfg.client_lanes:
             n = cfg.client_lanes
         elif not self.is_cuda:
@@ -399,6 +409,85 @@ class Federation:
             for ln in self.lanes:
                 if ln.stream is not None:
                     main.wait_stream(ln.stream)
+        return out
+
+    def _server_lane_worker(self, lane: ClientLane, r: int, G: torch.Tensor, w: Dict[int, float],
+                            keep: bool, out: dict) -> Iterator[None]:
+        """Server round on a lane: each of the lane's clients starts from the global model G,
+        trains its local epoch(s) and adds w_c * x_c into the lane's partial FedAvg sum (or, when
+        the anomaly filter needs every update, keeps a copy). Yields after every optimizer step."""
+        cfg = self.cfg
+        acc = out["acc"][lane.index]
+        for c in lane.clients:
+            with self._on(lane):
+                lane.flat.load_master(G)
+                if cfg.keep_optimizer_state and c in self.client_opt:
+                    lane.opt.load_state_dict(self.client_opt[c])
+                else:
+                    lane.opt.reset()
+                self.drift.attach(lane.opt, c)
+                loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
+            st = {"batches": 0, "tokens": 0, "examples": 0}
+            for e in range(cfg.local_epochs):
+                with self._on(lane):
+                    batches = self.train_batches(c, r, e)
+                for b in batches:
+                    lane.opt.lr = self.lr_at(r, st["batches"])
+                    with self._on(lane), self._client_rng(c):
+                        lane.trainer.step(b, loss_acc)
+                    st["batches"] += 1
+                    st["tokens"] += b.real_tokens
+                    st["examples"] += b.batch_size
+                    yield
+            st["loss_t"] = loss_acc
+            self.tokens_trained += st["tokens"]
+            if c in cfg.inject_slow:
+                time.sleep(cfg.inject_slow[c] / 1000.0)
+            with self._on(lane):
+                self.drift.after_train(c, lane.flat.master, self.lr_sum(r, st["batches"]))
+                self.drift.detach(lane.opt)
+                self._inject_byzantine(c, G, lane.flat)
+                if self.filter is not None:
+                    out["sk"][c], out["nr"][c] = self._update_stats(G, lane.flat)
+                out["losses"][c] = st
+                out["roots"][c] = (ops.merkle_root_deferred(lane.flat.master)
+                                   if self.ledger is not None else None)
+                if keep:
+                    out["trained"][c] = lane.flat.master.detach().clone()
+                else:
+                    ops.weighted_accumulate_(acc, lane.flat.master, float(w[c]))
+                if cfg.keep_optimizer_state:
+                    self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
+                                          for k, v in lane.opt.state_dict().items()}
+            yield
+
+    def _server_train_lanes(self, r: int, G: torch.Tensor, w: Dict[int, float], keep: bool) -> dict:
+        """All hosted clients of a server round, trained concurrently on the client lanes. The
+        FedAvg sum is accumulated per lane (fp32) and the lane partials are added in lane order
+        (deterministic for a given lane count)."""
+        if not hasattr(self, "_lane_acc") or len(self._lane_acc) != len(self.lanes):
+            self._lane_acc = [torch.zeros_like(self.flat.master) for _ in self.lanes]
+        out = {"sk": {}, "nr": {}, "losses": {}, "roots": {}, "trained": {}, "acc": self._lane_acc}
+        main = torch.cuda.current_stream(self.device) if self.is_cuda else None
+        for a in self._lane_acc:
+            a.zero_()
+        for ln in self.lanes:
+            if ln.stream is not None:
+                ln.stream.wait_stream(main)
+        with self.timer.phase("train"):
+            gens = [self._server_lane_worker(ln, r, G, w, keep, out) for ln in self.lanes]
+            while gens:
+                for g in list(gens):
+                    try:
+                        next(g)
+                    except StopIteration:
+                        gens.remove(g)
+            for ln in self.lanes:
+                if ln.stream is not None:
+                    main.wait_stream(ln.stream)
+        if not keep:
+            for a in self._lane_acc:
+                ops.weighted_accumulate_(self.acc, a, 1.0)
         return out
 
     # ================================ helpers ==================================================
@@ -759,10 +848,13 @@ class Federation:
     def _eval_global(self, r: int) -> EvalResult:
         with self.timer.phase("eval_global"):
             acc = torch.zeros(4, dtype=torch.float64, device=self.device)
-            for c, gb in self._global_eval_sets(r):
+            sets = self._global_eval_sets(r)
+            for c, gb in sets:
                 if gb:
                     self._bind_client(c)
                     acc += self.trainer.evaluate_device(gb)
+            if len(sets) > 1:
+                self._bind_client(self.local_clients[0])  # self.flat shows the first client again
             if not self.collective_free:
                 D.all_reduce_(acc)
             a = acc.cpu().tolist()
@@ -778,7 +870,19 @@ class Federation:
         need_copy = self.filter is not None and self.multi
         self.acc.zero_()
         w_all = counts / counts.sum()
-        for c in self.local_clients:
+        if self.lanes:
+            if self.verbose and cfg.reference_prints:
+                print("Training Started...", flush=True)
+            o = self._server_train_lanes(r, G, {c: float(w_all[c]) for c in self.local_clients},
+                                         keep=self.filter is not None)
+            if self.verbose and cfg.reference_prints:
+                print("Training Finished.", flush=True)
+            sk, nr, losses, trained = o["sk"], o["nr"], o["losses"], o["trained"]
+            for c in self.local_clients:
+                root = ops.root_bytes(o["roots"][c]).hex() if o["roots"][c] is not None else ""
+                recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
+                             "verdict": "accept", "metrics": {"examples": losses[c]["examples"]}})
+        for c in ([] if self.lanes else self.local_clients):
             self._activate(c, master=G)
             if self.verbose and cfg.reference_prints:
                 print("Training Started...", flush=True)
@@ -812,8 +916,24 @@ class Federation:
                 ops.weighted_accumulate_(self.acc, trained[c], float(w[c]))
             for x in recs:
                 x["verdict"] = v.verdict(x["client"])
+        absent = []
         with self.timer.phase("comm"):
-            if cfg.server_wire_dtype == "bf16" and self.rt.distributed:
+            if self.server_mbox is not None:
+                wloc = float(sum(w_all[c] for c in self.local_clients))
+                g_new, minfo = self.server_mbox.reduce(r, self.acc, wloc)
+                self.acc.copy_(g_new)
+                wire_bytes = minfo["bytes_sent"]
+                absent = minfo["absent_ranks"]
+                for g in self.server_mbox.take_records():
+                    if g["kind"] == "recv":
+                        recs.append({"client": -1, "kind": "verify", "root": g["root"],
+                                     "verdict": "accept" if g["ok"] else "reject",
+                                     "ts": float(r) + 0.5,
+                                     "metrics": {"sender_rank": -g["client"] - 1,
+                                                 "receiver_rank": self.rt.rank,
+                                                 "version": g["version"], "src_round": g["src_round"]}})
+                self._server_live = minfo
+            elif cfg.server_wire_dtype == "bf16" and self.rt.distributed:
                 # delta coding: each rank reduces sum_{k local} w_k (x_k - G), bf16 on the wire
                 wloc = float(sum(w[c] for c in self.local_clients)) if self.filter is not None \
                     else float(sum(w_all[c] for c in self.local_clients))
@@ -839,15 +959,22 @@ class Federation:
                     a = t.cpu().tolist()
                     e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
                     loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
-                client_metrics = [x for part in D.all_gather_object(loc) for x in part]
+                client_metrics = self._gather_metrics(loc)
         agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
         ge = self._eval_global(r) if cfg.eval_global else None
         train_loss = self._reduce_train_loss(losses)
-        self._ledger_round(r, recs, {"kind": "global", "root": self._merkle() if self.ledger else "",
-                                     "rejected": sorted(v.rejected)})
-        return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
-                "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
-                "client_metrics": client_metrics, "bytes_sent": float(wire_bytes)}
+        extra = {"kind": "global", "root": self._merkle() if self.ledger else "",
+                 "rejected": sorted(v.rejected)}
+        if self.server_mbox is not None:
+            extra.update(absent_ranks=absent, live_weight=self._server_live["live_weight"])
+        self._ledger_round(r, recs, extra)
+        out = {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
+               "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
+               "client_metrics": client_metrics, "bytes_sent": float(wire_bytes)}
+        if self.server_mbox is not None:
+            out.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
+                       dead_peers=sorted(self.server_mbox.dead))
+        return out
 
     @property
     def _gossip_roots(self) -> bool:
@@ -1037,7 +1164,8 @@ class Federation:
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
                "dead_peers": res.get("dead_peers", []),
-               **{k: res[k] for k in ("mixed", "stale_rounds", "torn", "rejected_msgs") if k in res},
+               **{k: res[k] for k in ("mixed", "stale_rounds", "torn", "rejected_msgs",
+                                      "absent_ranks", "live_weight") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
         if self.is_cuda:
@@ -1136,6 +1264,8 @@ class Federation:
         self._resolve_eval()
         if self.gossip is not None:
             self.gossip.drain()
+        if self.server_mbox is not None:
+            self.server_mbox.drain()
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
         self.timer.resolve(block=True)

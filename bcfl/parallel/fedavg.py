@@ -1,0 +1,144 @@
+"""Server FedAvg that survives dead ranks: the weighted sum over one-sided mailboxes.
+
+Reference: Flower's ``FedAvg`` (``src/Servercase/server_IID_IMDB.py:205-209``) runs with
+``accept_failures=True`` by default — a client that fails a round is left out of that round's
+aggregate and the weights are re-normalised over the results that arrived (SURVEY.md §5.3 item
+3). An RCCL all-reduce cannot do that: one exited rank blocks every survivor in the collective
+until the process group times out.
+
+Here every rank is its own aggregator:
+
+1. it adds its hosted clients' models into a partial sum ``S_r = sum_{c on r} w_c x_c`` (global
+   example-count weights) and posts ``S_r`` with its weight ``W_r = sum_{c on r} w_c`` (in the
+   header) and the payload's SHA-256 Merkle root into every peer's inbox (one-sided copies on
+   side streams, :mod:`bcfl.parallel.mailbox`);
+2. it waits — bounded by ``timeout_s`` — for round r's post of every rank it still counts as
+   live, verifies each payload's root, and declares the ranks that did not post (or posted a
+   payload that fails verification) absent;
+3. the new global model is ``G = sum_{r live} S_r / sum_{r live} W_r`` summed in rank order, so
+   every survivor that saw the same live set computes the bit-identical G; absentees stay out
+   (dead) for the rest of the run and are recorded in each rank's ledger block.
+
+With every rank live, G equals the all-reduce result (up to the fp32 summation order). Payloads
+are fp32 (exact partial sums); inboxes cost 2 slots x model bytes per peer (7 x 0.87 GB for
+BERT-base on an 8-GPU node — small against 288 GB of HBM).
+"""
+from __future__ import annotations
+
+import struct
+import time
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import ops
+from . import dist as D
+from .mailbox import MailboxTransport, Snapshot
+
+
+def _f2i(x: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", float(x)))[0]
+
+
+def _i2f(i: int) -> float:
+    return struct.unpack("<d", struct.pack("<q", int(i)))[0]
+
+
+class MailboxFedAvg:
+    def __init__(self, numel: int, device: torch.device, timeout_s: float = 120.0,
+                 verify: bool = True, rank: Optional[int] = None, world: Optional[int] = None):
+        rt = D.runtime()
+        self.rank = rt.rank if rank is None else rank
+        self.world = rt.world if world is None else world
+        self.peers = [r for r in range(self.world) if r != self.rank]
+        self.numel, self.device = numel, device
+        self.timeout_s = float(timeout_s)
+        self.verify = verify
+        # mailbox "clients" are ranks here: rank r posts its partial sum as client id r
+        self.transport = MailboxTransport(numel, torch.float32, device, listen=self.peers,
+                                          send_plan=[(self.rank, p) for p in self.peers],
+                                          rank=self.rank, world=self.world)
+        z = lambda: torch.zeros(numel, dtype=torch.float32, device=device)  # noqa: E731
+        self.send_buf = [z(), z()]
+        self.stage = {p: z() for p in self.peers}
+        self.dead: set = set()
+        self.records: List[dict] = []
+        self.bytes_posted = 0
+
+    def reduce(self, r: int, partial: torch.Tensor, w_local: float) -> Tuple[torch.Tensor, Dict]:
+        """Round r: post ``partial`` (this rank's weighted sum, fp32 flat) with weight
+        ``w_local``; return (G, info) with G the re-normalised sum over the live ranks."""
+        v = r + 1
+        slot = v % 2
+        tr = self.transport
+        if tr.is_cuda:
+            tr.wait_slot_free(self.rank, slot)
+        buf = self.send_buf[slot]
+        buf.copy_(partial)
+        root = ops.merkle_root_deferred(buf) if self.verify else None
+        snap = Snapshot(v, r, _f2i(w_local), buf.numel() * 4, b"\0" * 32)
+        rd = root
+        if rd is not None and not torch.is_tensor(rd):
+            snap.root, rd = bytes(rd), None
+        b0 = tr.bytes_posted
+        tr.post(self.rank, buf, snap, rd)
+        self.records.append({"client": -(self.rank + 1), "kind": "update", "version": v,
+                             "root_t": root})
+        # ---- wait for round r from every rank still counted live ----------------------------
+        need = [p for p in self.peers if p not in self.dead]
+        got: Dict[int, Snapshot] = {}
+        t0 = time.perf_counter()
+        while True:
+            left = [p for p in need if p not in got]
+            if not left:
+                break
+            got.update(tr.fetch_exact({p: v for p in left}, self.stage))
+            if all(p in got for p in need) or time.perf_counter() - t0 > self.timeout_s:
+                break
+            time.sleep(0.0005)
+        absent = sorted(p for p in need if p not in got)
+        ok = {}
+        if got and self.verify:
+            fs = tr.fetch_stream
+            ctx = torch.cuda.stream(fs) if fs is not None else None
+            if ctx is not None:
+                ctx.__enter__()
+            try:
+                for p in got:
+                    ok[p] = ops.root_bytes(ops.merkle_root_deferred(self.stage[p])) == got[p].root
+            finally:
+                if ctx is not None:
+                    ctx.__exit__(None, None, None)
+            if fs is not None:
+                torch.cuda.current_stream(self.device).wait_stream(fs)
+        for p, sn in got.items():
+            good = ok.get(p, True)
+            self.records.append({"client": -(p + 1), "kind": "recv", "version": sn.version,
+                                 "root": sn.root.hex(), "ok": good, "src_round": sn.round})
+            if not good:
+                absent.append(p)
+        absent = sorted(set(absent))
+        self.dead |= set(absent)
+        # ---- G = sum_{live} S_r / sum_{live} W_r, in rank order -------------------------------
+        live = sorted([self.rank] + [p for p in got if p not in absent])
+        out = torch.zeros_like(partial)
+        wsum = 0.0
+        for q in live:
+            src = partial if q == self.rank else self.stage[q]
+            ops.axpby_(out, src, 1.0, 1.0)
+            wsum += w_local if q == self.rank else _i2f(got[q].steps)
+        if wsum > 0 and abs(wsum - 1.0) > 1e-12:
+            ops.scale_(out, 1.0 / wsum)
+        self.bytes_posted += tr.bytes_posted - b0
+        return out, {"live_ranks": live, "absent_ranks": absent, "live_weight": wsum,
+                     "bytes_sent": float(tr.bytes_posted - b0)}
+
+    def take_records(self) -> List[dict]:
+        out, self.records = self.records, []
+        return out
+
+    def drain(self):
+        self.transport.drain()
+
+    def close(self):
+        self.transport.close()

@@ -318,6 +318,14 @@ def _portable_records(recs: List[dict]) -> List[dict]:
     return out
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 @torch.no_grad()
 def _delta_encode_ref(x: torch.Tensor, ref: torch.Tensor, out: torch.Tensor):
     q = (x - ref).to(out.dtype)
@@ -447,7 +455,10 @@ class MailboxGossip:
         Merkle root against the sender's commitment, adopt the good ones."""
         import time as _time
         want = {j: self.applied[j] for j in self.remote_needed}
-        got = self.transport.fetch(want, self.stage)
+        tr = self.transport
+        fs = tr.fetch_stream  # GPU: the whole receive path runs on the transport's side stream
+        after = getattr(self, "_mix_done", None)
+        got = tr.fetch(want, self.stage, after=after)
         if not self.async_gossip:
             t0 = _time.perf_counter()
             need = {j for j in self.remote_needed if j not in self.dead}
@@ -458,18 +469,20 @@ class MailboxGossip:
                 _time.sleep(0.0005)
                 # re-fetch into scratch buffers: a torn re-fetch must not overwrite the complete
                 # snapshot already staged for j (got[j] keeps describing stage[j])
-                more = self.transport.fetch({j: max(self.applied[j], got[j].version if j in got else 0)
-                                             for j in need - have}, self.scratch)
+                more = tr.fetch({j: max(self.applied[j], got[j].version if j in got else 0)
+                                 for j in need - have}, self.scratch)
                 for j in more:
                     self.stage[j], self.scratch[j] = self.scratch[j], self.stage[j]
                 got.update(more)
                 have |= {j for j, s in more.items() if s.round >= round_idx}
-        self.torn = self.transport.torn
+        self.torn = tr.torn
         ok = {}
         if got and self.verify:
-            roots = {j: ops.merkle_root_deferred(self.stage[j]) for j in got}
-            for j, rt in roots.items():
-                ok[j] = ops.root_bytes(rt) == got[j].root
+            # re-hash on the fetch stream: the root readback waits only for this stream
+            with (torch.cuda.stream(fs) if fs is not None else _nullctx()):
+                roots = {j: ops.merkle_root_deferred(self.stage[j]) for j in got}
+                for j, rt in roots.items():
+                    ok[j] = ops.root_bytes(rt) == got[j].root
         for j, snap in got.items():
             good = ok.get(j, True)
             self.records.append({"client": j, "kind": "recv", "version": snap.version,
@@ -505,7 +518,13 @@ class MailboxGossip:
         self.publish(round_idx, steps)
         self.collect(round_idx)
         self._age_out(round_idx)
+        fs = self.transport.fetch_stream
+        if fs is not None:  # the mix reads what the fetch stream wrote
+            torch.cuda.current_stream(self.device).wait_stream(fs)
         self.mix(self.live_matrix(W), param_out)
+        if fs is not None:  # the next fetch may overwrite the buffers this mix read after this
+            self._mix_done = torch.cuda.Event()
+            self._mix_done.record(torch.cuda.current_stream(self.device))
         ages = [round_idx - self.replica_round[j] for j in self.remote_needed if j not in self.dead]
         return {"mixed": 1.0, "stale_rounds": float(np.mean(ages)) if ages else 0.0,
                 "bytes_sent": float(self.transport.bytes_posted - b0),

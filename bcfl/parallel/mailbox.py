@@ -214,6 +214,17 @@ class MailboxTransport:
         for ev in self.posted.pop((c, slot), []):
             torch.cuda.current_stream(self.device).wait_event(ev)
 
+    def post_to(self, c: int, payload: torch.Tensor, snap: Snapshot, dsts: Sequence[int],
+                root_dev: Optional[torch.Tensor] = None):
+        """:meth:`post` restricted to the destination ranks ``dsts`` (information-passing
+        measurements: one destination at a time vs all at once)."""
+        keep = self.outbox.get(c, [])
+        self.outbox[c] = [(d, b) for d, b in keep if d in set(dsts)]
+        try:
+            self.post(c, payload, snap, root_dev)
+        finally:
+            self.outbox[c] = keep
+
     def post(self, c: int, payload: torch.Tensor, snap: Snapshot,
              root_dev: Optional[torch.Tensor] = None):
         """Publish ``payload`` (wire-encoded, ``numel`` elements) as version ``snap.version`` of
@@ -287,11 +298,27 @@ class MailboxTransport:
         self.posted.clear()
 
     # ------------------------------------------------------------------ receiver
+    @property
+    def fetch_stream(self):
+        """Side stream of the receive path (GPU): header reads, payload copies and the
+        receiver's verification hashing run here, so polling a mailbox never waits for (drains)
+        the compute stream; the host waits only for this stream's small, already-issued work."""
+        if not self.is_cuda:
+            return None
+        if getattr(self, "_fs", None) is None:
+            self._fs = torch.cuda.Stream(device=self.device)
+        return self._fs
+
     def headers(self, js: Sequence[int]) -> Dict[int, np.ndarray]:
-        """Both slot headers of every inbox in ``js`` (one device->host read)."""
+        """Both slot headers of every inbox in ``js`` (one device->host read, on the fetch
+        stream: the read waits for nothing queued on the compute stream)."""
         if not js:
             return {}
-        h = torch.stack([self.inbox[j].hdr for j in js]).cpu().numpy()
+        if self.is_cuda:
+            with torch.cuda.stream(self.fetch_stream):
+                h = torch.stack([self.inbox[j].hdr for j in js]).cpu().numpy()
+        else:
+            h = torch.stack([self.inbox[j].hdr for j in js]).cpu().numpy()
         return {j: h[i] for i, j in enumerate(js)}
 
     @staticmethod
@@ -304,17 +331,29 @@ class MailboxTransport:
                                     words_to_root(h[s, W_ROOT:W_ROOT + 4])))
         return best
 
-    def fetch(self, want: Dict[int, int], out: Dict[int, torch.Tensor]) -> Dict[int, Snapshot]:
+    def fetch(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
+              after: Optional["torch.cuda.Event"] = None) -> Dict[int, Snapshot]:
         """For every inbox j with a complete version newer than ``want[j]``, copy it into
-        ``out[j]`` (stream-ordered) and return the validated snapshots; torn reads are dropped."""
+        ``out[j]`` and return the validated snapshots; torn reads are dropped.
+
+        GPU: everything runs on :attr:`fetch_stream`, first ordered after ``after`` (the event
+        after which the ``out`` buffers are no longer read, e.g. the previous mix); a consumer on
+        another stream must wait for it (``stream.wait_stream(transport.fetch_stream)``)."""
         js = list(want)
+        fs = self.fetch_stream
+        if fs is not None and after is not None:
+            fs.wait_event(after)
         first = self.headers(js)
         picked: Dict[int, Tuple[int, Snapshot]] = {}
         for j in js:
             nw = self.newest(first[j])
             if nw is not None and nw[1].version > want[j]:
                 picked[j] = nw
-                out[j].copy_(self.inbox[j].slots[nw[0]], non_blocking=self.is_cuda)
+                if fs is not None:
+                    with torch.cuda.stream(fs):
+                        out[j].copy_(self.inbox[j].slots[nw[0]], non_blocking=True)
+                else:
+                    out[j].copy_(self.inbox[j].slots[nw[0]])
         if not picked:
             return {}
         second = self.headers(list(picked))  # stream-ordered after the payload copies
@@ -325,6 +364,44 @@ class MailboxTransport:
                 good[j] = snap
             else:
                 self.torn += 1
+        if fs is not None:  # device-side dependency only: the caller's stream reads out[] later
+            torch.cuda.current_stream(self.device).wait_stream(fs)
+        return good
+
+    def fetch_exact(self, want: Dict[int, int], out: Dict[int, torch.Tensor]) -> Dict[int, Snapshot]:
+        """Like :meth:`fetch` but for EXACTLY version ``want[j]`` (a slot whose begin == end ==
+        that version): round-synchronous protocols (server FedAvg over mailboxes) need round r's
+        post even when the sender has already posted round r + 1 into its other slot."""
+        js = list(want)
+        fs = self.fetch_stream
+        first = self.headers(js)
+        picked: Dict[int, Tuple[int, Snapshot]] = {}
+        for j in js:
+            h = first[j]
+            for slot in (0, 1):
+                v = int(h[slot, W_BEGIN])
+                if v == want[j] and v == int(h[slot, W_END]):
+                    picked[j] = (slot, Snapshot(v, int(h[slot, W_ROUND]), int(h[slot, W_STEPS]),
+                                                int(h[slot, W_BYTES]),
+                                                words_to_root(h[slot, W_ROOT:W_ROOT + 4])))
+                    if fs is not None:
+                        with torch.cuda.stream(fs):
+                            out[j].copy_(self.inbox[j].slots[slot], non_blocking=True)
+                    else:
+                        out[j].copy_(self.inbox[j].slots[slot])
+                    break
+        if not picked:
+            return {}
+        second = self.headers(list(picked))
+        good = {}
+        for j, (slot, snap) in picked.items():
+            h = second[j]
+            if int(h[slot, W_BEGIN]) == snap.version and int(h[slot, W_END]) == snap.version:
+                good[j] = snap
+            else:
+                self.torn += 1
+        if fs is not None:
+            torch.cuda.current_stream(self.device).wait_stream(fs)
         return good
 
     def close(self):

@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
     ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
+    ap.add_argument("--no-info-passing", action="store_true",
+                    help="skip the post-run information-passing measurement (N > 1)")
     ap.add_argument("--global-test-samples", type=int, default=0,
                     help="override the global evaluation draw (experiments only; 0 = preset)")
     ap.add_argument("--micro-batches", type=int, default=0,
@@ -168,6 +170,13 @@ def main():
     # peer over xGMI), read before finish() closes the transport
     tr = getattr(fed.gossip, "transport", None)
     p2p = tr.post_stats() if tr is not None and hasattr(tr, "post_stats") else None
+    info = None
+    if rt.world > 1 and not a.no_info_passing:
+        # outside the timed rounds: one client's model (the wire payload of the gossip engine)
+        # from rank 0 to every peer over the mailbox transport, sequential (sync) vs concurrent
+        # (async), measured and predicted, before / after PageRank removal
+        from bcfl.trust.infopass import measure
+        info = measure(fed.flat.numel, sources=[0], iters=3)
     fed.finish()
     if rt.is_main:
         rec = {
@@ -220,6 +229,7 @@ def main():
                        "gossip_transport": fed.transport},
             "checkpoints": {"saved": ck.saved if ck else 0, "skipped": ck.skipped if ck else 0},
             "p2p_post_measured": p2p,
+            "info_passing": info,
             "ledger": {"height": len(fed.ledger) if fed.ledger else 0,
                        "audit": fed.ledger_audit,
                        "rejected_msgs": last.get("rejected_msgs")},

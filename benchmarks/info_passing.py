@@ -80,10 +80,14 @@ def run(numel: int, iters: int = 3, probe_bytes: int = 64 << 20) -> dict:
     return res
 
 
-def _cpu_worker(rank, world, numel, out):
+def _cpu_worker(rank, world, numel, out, transport="rccl"):
     from bcfl.parallel import dist as D
     D.init_runtime("cpu", "gloo")
-    r = run(numel, 2, 1 << 18)
+    if transport == "mailbox":
+        from bcfl.trust.infopass import measure
+        r = measure(numel, iters=2)
+    else:
+        r = run(numel, 2, 1 << 18)
     if rank == 0:
         with open(out, "w") as fh:
             json.dump(r, fh)
@@ -96,6 +100,8 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--json", default=None)
     ap.add_argument("--cpu-world", type=int, default=0, help="gloo rehearsal with this many CPU ranks")
+    ap.add_argument("--transport", default="mailbox", choices=("mailbox", "rccl"),
+                    help="mailbox: one-sided posts (what the gossip engine uses); rccl: send/recv")
     a = ap.parse_args(argv)
     numel = a.numel
     if not numel:
@@ -110,19 +116,25 @@ def main(argv=None):
         from dist_utils import run_world
         with tempfile.TemporaryDirectory() as td:
             out = os.path.join(td, "r.json")
-            run_world(_cpu_worker, a.cpu_world, td, min(numel, 1 << 20), out)
+            run_world(_cpu_worker, a.cpu_world, td, min(numel, 1 << 20), out, a.transport)
             res = json.load(open(out))
         del mp
     else:
         from bcfl.parallel import dist as D
         D.init_runtime("auto", "auto")
-        res = run(numel, a.iters)
+        if a.transport == "mailbox":
+            from bcfl.trust.infopass import measure
+            res = measure(numel, iters=a.iters)
+        else:
+            res = run(numel, a.iters)
         if not D.runtime().is_main:
             return 0
-    for s in res["sources"]:
-        print(f"source {s['source']}: measured sync {s['measured_sync_s'] * 1e3:.2f} ms async "
-              f"{s['measured_async_s'] * 1e3:.2f} ms | predicted sync {s['predicted_sync_s'] * 1e3:.2f} ms "
-              f"async {s['predicted_async_s'] * 1e3:.2f} ms")
+    for s in res["sources"] + res.get("after_pagerank_removal", []):
+        tag = f" (without {s['excluded']})" if "excluded" in s else ""
+        print(f"source {s['source']}{tag}: measured sync {s['measured_sync_s'] * 1e3:.2f} ms async "
+              f"{s['measured_async_s'] * 1e3:.2f} ms | predicted sync "
+              f"{s.get('predicted_sync_s', float('nan')) * 1e3:.2f} ms async "
+              f"{s.get('predicted_async_s', float('nan')) * 1e3:.2f} ms")
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(res, fh, indent=1)

@@ -275,3 +275,44 @@ def test_bench_path_world8_anomaly_filter_consensus(tmp_path):
                     {"anomaly_filter": "both", "wire_dtype": "bf16"})
     assert all(bool(r["consensus"]) for r in res)
     assert len({r["tip"] for r in res}) == 1
+
+
+def _server_liveness_worker(rank, world, out, exit_after):
+    from bcfl.fl import Federation
+    fed = Federation(_cfg("server", out, num_clients=3, num_rounds=4, server_transport="mailbox",
+                          server_timeout_s=3.0), verbose=False)
+    rounds = exit_after if rank == world - 1 else fed.cfg.num_rounds
+    for r in range(rounds):
+        fed.run_round(r)
+    if rank == world - 1:   # this rank "crashes": leaves without finishing, posts nothing more
+        return {"rounds": torch.tensor(rounds)}
+    fed.finish(audit=False)
+    blocks = [b for b in fed.ledger.blocks() if b["kind"] == "global"]
+    import json as _json
+    absent = [_json.loads(b["payload"] or "{}").get("absent_ranks", []) for b in blocks]
+    return {"rounds": torch.tensor(len(fed.history)), "G": fed.global_master.clone(),
+            "live_w": torch.tensor([h["live_weight"] for h in fed.history], dtype=torch.float64),
+            "absent": [list(a) for a in absent],
+            "acc": torch.tensor([h["global_acc"] for h in fed.history])}
+
+
+def test_server_mailbox_fedavg_survives_a_dead_rank(tmp_path):
+    """Flower FedAvg accept_failures semantics without a server: rank 2 stops after round 1; the
+    survivors finish every round, leave it out, re-normalise the weights over the live ranks
+    (3 equal clients: 1 -> 2/3) and record the absentee in their ledgers."""
+    res = run_world(_server_liveness_worker, 3, str(tmp_path / "d"), str(tmp_path / "d"), 2)
+    assert int(res[2]["rounds"]) == 2
+    for r in res[:2]:
+        assert int(r["rounds"]) == 4 and torch.isfinite(r["G"]).all()
+        lw = r["live_w"].tolist()
+        assert lw[:2] == pytest.approx([1.0, 1.0]) and lw[2:] == pytest.approx([2 / 3, 2 / 3])
+        assert r["absent"][:2] == [[], []] and r["absent"][2] == [2]
+    assert torch.equal(res[0]["G"], res[1]["G"])   # same live set -> bit-identical global model
+
+
+def test_server_mailbox_equals_allreduce_when_all_live(tmp_path):
+    a = run_world(_fed_worker, 2, str(tmp_path / "a"), "server", str(tmp_path / "a"),
+                  {"server_transport": "mailbox"})
+    b = run_world(_fed_worker, 2, str(tmp_path / "b"), "server", str(tmp_path / "b"), {})
+    assert torch.equal(a[0]["master"], a[1]["master"])
+    torch.testing.assert_close(a[0]["master"], b[0]["master"], atol=1e-6, rtol=0)

@@ -361,3 +361,20 @@ def test_checkpoint_jobs_sharing_a_source_are_written_once(tmp_out):
     ck.save([], jobs=[([d[0]], fed.flat.master), ([d[1]], fed.flat.master)])
     sd2 = read_safetensors(os.path.join(d[1], "model.safetensors"))
     assert not torch.equal(sd2[next(iter(sd2))], sd[1][next(iter(sd2))])
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_server_lanes_match_sequential(tmp_out, lanes):
+    """Server FedAvg with the hosted clients trained concurrently on client lanes (each from the
+    global model, per-lane partial FedAvg sums) reproduces one-lane training up to the fp32
+    summation order of the lane partials."""
+    kw = dict(mode="server", num_clients=4, num_rounds=2, dropout=0.1)
+    a = Federation(_cfg(tmp_out + "_a", client_lanes=1, **kw), verbose=False)
+    ha = a.run()
+    D.set_runtime_for_tests(None)
+    b = Federation(_cfg(tmp_out + "_b", client_lanes=lanes, **kw), verbose=False)
+    assert len(b.lanes) == lanes
+    hb = b.run()
+    assert float((a.global_master - b.global_master).abs().max()) < 1e-6
+    assert [h["train_loss"] for h in ha] == pytest.approx([h["train_loss"] for h in hb], rel=1e-5)
+    assert [h["global_acc"] for h in ha] == [h["global_acc"] for h in hb]

@@ -165,3 +165,31 @@ def test_gpu_micro_batch_clients_match_full_batch(tmp_path):
     assert lb == pytest.approx(la, rel=2e-2)
     assert torch.isfinite(mb_).all()
     assert float((ma - mb_).abs().max()) < 5e-3
+
+
+def _run_server(tmp, lanes):
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    cfg = FLConfig(mode="server", model="bert-base-2l", dataset="imdb", num_clients=4,
+                   num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                   out_dir=tmp, reference_prints=False, client_lanes=lanes, overlap_wgrad=False,
+                   ledger=True, save_every=0, dropout=0.1)
+    fed = Federation(cfg, verbose=False)
+    assert len(fed.lanes) == lanes
+    h = fed.run()
+    torch.cuda.synchronize()
+    out = (fed.global_master.cpu(), [r["train_loss"] for r in h], [r["global_acc"] for r in h])
+    D.set_runtime_for_tests(None)
+    return out
+
+
+def test_gpu_server_lanes_close_to_sequential(tmp_path):
+    """Server FedAvg with the hosted clients on concurrent lanes (per-lane partial sums) tracks
+    one-lane training within the lanes tolerance (fp32 sum order of the lane partials)."""
+    a = _run_server(str(tmp_path / "a"), 1)
+    b = _run_server(str(tmp_path / "b"), 3)
+    assert torch.isfinite(b[0]).all()
+    assert float((a[0] - b[0]).abs().max()) < 2e-4
+    assert a[1] == pytest.approx(b[1], rel=1e-3)

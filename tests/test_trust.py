@@ -2,6 +2,7 @@
 import json
 
 import numpy as np
+import torch
 import pytest
 
 from bcfl.trust import graph as G
@@ -155,3 +156,25 @@ def test_plots_from_metrics(tmp_path):
     assert plots.main(["--metrics", str(m), "--report", str(rep), "--out", str(tmp_path / "figs")]) == 0
     for f in ("global_accuracy.png", "round_time.png", "info_passing.png"):
         assert (tmp_path / "figs" / f).stat().st_size > 1000
+
+
+def _infopass_cpu_worker(rank, world):
+    from bcfl.parallel import dist as D
+    from bcfl.trust.infopass import measure
+    D.init_runtime("cpu", "gloo")
+    r = measure(1 << 16, iters=2)
+    return {"n": torch.tensor(len(r["sources"])), "bw": torch.tensor(r["bw_MBps"]),
+            "pred": torch.tensor([s.get("predicted_async_s", -1.0) for s in r["sources"]])}
+
+
+def test_info_passing_mailbox_gloo(tmp_path):
+    """Sync vs async information passing measured over the mailbox transport (gloo + /dev/shm
+    rehearsal of the xGMI path): every source measured, bandwidth matrix filled, analytical
+    prediction evaluated on it."""
+    from dist_utils import run_world
+    res = run_world(_infopass_cpu_worker, 3, str(tmp_path))
+    r = res[0]
+    assert int(r["n"]) == 3
+    bw = r["bw"]
+    assert bool((bw[~torch.eye(3, dtype=torch.bool)] > 0).all())
+    assert bool((r["pred"] > 0).all())
