@@ -304,6 +304,13 @@ PRESETS: Dict[str, Dict[str, Any]] = {
                                                 max_seq_len=512, lr=2e-4),
 }
 
+# The random-init learning protocol of baseline3_learnable applied to BASELINE configs 2 and 4
+# (timing records of those configs carry an accuracy that means something).
+_LEARNABLE = dict(lr=2e-5, lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
+                  global_test_samples=1000, drift_correction="auto")
+PRESETS["baseline2_learnable"] = {**PRESETS["baseline2_bert_server_iid"], **_LEARNABLE}
+PRESETS["baseline4_learnable"] = {**PRESETS["baseline4_biobert_serverless_noniid_trust"], **_LEARNABLE}
+
 # Reference-faithful ("_compat") variants of the three scripts whose data handling differs from
 # what their names say. The un-suffixed presets above keep the INTENDED semantics (a real
 # Non-IID split); these reproduce what the scripts actually run.

@@ -668,6 +668,11 @@ bool gemm_native_ok(int64_t M, int64_t N, int64_t K, bool nn, bool accum) {
 }
 
 // ------------------------------------------------------------------------------------------------
+namespace {
+bool g_wgrad_g8 = false;
+}
+void set_wgrad_kernel(bool g8) { g_wgrad_g8 = g8; }
+
 // dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
 std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   TORCH_CHECK(g.is_cuda() && x.is_cuda(), "wgrad: GPU tensors required");
@@ -677,7 +682,15 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   TORCH_CHECK(g.stride(0) % 8 == 0 && x.stride(0) % 8 == 0, "wgrad: 16-byte aligned rows");
   const int M = g.size(0), N = g.size(1), K = x.size(1);
   int Mc = 0;
-  const int S = bcfl::wgrad_splits(M, N, K, &Mc);
+  // the 8-phase kernel (gemm8.hip) for 256-multiple shapes, the K9 kernel (gemm.hip) otherwise
+  // kernel choice: BCFL_WGRAD_G8=0/1 (read per call: A/B switchable at run time) overrides the
+  // regime default set by set_wgrad_kernel() (ops.set_wgrad_overlap: g8 when the weight gradients
+  // run on the side stream beside the dgrad chain, K9 when concurrent lanes fill the GPU)
+  const char* env_g8 = std::getenv("BCFL_WGRAD_G8");
+  const bool use_g8 = env_g8 && *env_g8 ? env_g8[0] != '0' : g_wgrad_g8;
+  int S = use_g8 ? bcfl::wgrad_g8_splits(M, N, K, &Mc) : 0;
+  const bool g8 = S >= 1;
+  if (!g8) S = bcfl::wgrad_splits(M, N, K, &Mc);
   TORCH_CHECK(S >= 1, "wgrad: N and K must be multiples of 128");
   auto out = torch::empty({N, K}, g.options());
   Tensor part;
@@ -687,11 +700,12 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   Tensor db, dbp;
   if (with_bias) {
     db = torch::empty({N}, g.options());
-    dbp = torch::empty({S, N}, g.options().dtype(torch::kFloat));
+    dbp = torch::empty({g8 ? std::max(S, bcfl::wgrad_g8_bias_parts(M)) : S, N},
+                       g.options().dtype(torch::kFloat));
     p.dbias_part = dbp.data_ptr<float>();
     p.dbias = db.data_ptr();
   }
-  check_rc(bcfl::launch_wgrad(p, stream()), "wgrad");
+  check_rc(g8 ? bcfl::launch_wgrad_g8(p, stream()) : bcfl::launch_wgrad(p, stream()), "wgrad");
   if (with_bias) return {out, db};
   return {out};
 }
@@ -777,6 +791,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_dgrad", &linear_dgrad);
   m.def("wgrad_bias", &wgrad_bias);
   m.def("gemm8", &gemm8);
+  m.def("set_wgrad_kernel", &set_wgrad_kernel);
   m.def("linear_dgrad_acc", &linear_dgrad_acc);
   m.def("linear_fwd_acc", &linear_fwd_acc);
   m.def("gemm_native_ok", &gemm_native_ok);

@@ -212,12 +212,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            int N, int K, bf16_t* __restrict__ out,
                                                            int64_t ldo, int main_blocks,
                                                            const float* __restrict__ bpart,
-                                                           bf16_t* __restrict__ dbias) {
+                                                           bf16_t* __restrict__ dbias, int SB) {
   if ((int)blockIdx.x >= main_blocks) {  // bias columns (block-uniform branch)
     const int n = (blockIdx.x - main_blocks) * 256 + threadIdx.x;
     if (n >= N) return;
     float a = 0.f;
-    for (int s = 0; s < S; ++s) a += bpart[(int64_t)s * N + n];
+    for (int s = 0; s < SB; ++s) a += bpart[(int64_t)s * N + n];
     dbias[n] = f2bf(a);
     return;
   }
@@ -238,6 +238,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 }
 
 }  // namespace
+
+int launch_wgrad_reduce(const float* part, int S, int N, int K, void* out, int64_t ldo,
+                        const float* bpart, void* dbias, hipStream_t s, int SB) {
+  const int64_t n4 = (int64_t)N * K / 4;
+  const int main_blocks = part ? (int)((n4 + 255) / 256) : 0;  // part == nullptr: bias only
+  if (SB <= 0) SB = S;
+  const int bias_blocks = bpart ? (N + 255) / 256 : 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(main_blocks + bias_blocks)), dim3(256), 0,
+                     s, part, S, N, K, reinterpret_cast<bf16_t*>(out), ldo, main_blocks, bpart,
+                     reinterpret_cast<bf16_t*>(dbias), SB);
+  return 0;
+}
 
 int wgrad_splits(int M, int N, int K, int* Mc) {
   if (N % BT || K % BT || M <= 0) return -1;
@@ -275,7 +287,7 @@ int launch_wgrad(const WgradParams& p, hipStream_t s) {
     const int bias_blocks = p.dbias_part ? (p.N + 255) / 256 : 0;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(main_blocks + bias_blocks)), dim3(256),
                        0, s, p.part, p.S, p.N, p.K, reinterpret_cast<bf16_t*>(p.out), p.ldo,
-                       main_blocks, p.dbias_part, reinterpret_cast<bf16_t*>(p.dbias));
+                       main_blocks, p.dbias_part, reinterpret_cast<bf16_t*>(p.dbias), p.S);
   }
   return 0;
 }

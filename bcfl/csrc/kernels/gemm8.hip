@@ -42,6 +42,8 @@
 // Epilogues (EPI_*) are applied while the 256 x BN tile streams out through a per-wave LDS slab
 // (16-byte row segments): bias, bias + activation (pre-activation saved), activation' (dgrad of
 // the layer after an activation), accumulate into C (beta = 1), or fp32 split-K partials.
+#include <cstdlib>
+
 #include "act.h"
 #include "common.h"
 #include "kernels.h"
@@ -189,16 +191,21 @@ struct G8RowRd {
 // drain of the DMA pipeline) in front of every one. hipcc does not count asm loads, so every
 // phase waits lgkmcnt(0) itself after its first barrier and then marks the fragments written
 // (g8_fence) before the MFMAs may read them.
+template <int OFF>
 __device__ __forceinline__ s16x4_t g8_tr_read(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
   s16x4_t v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
   return v;
 }
 
+// Transposed-read fragments of a COL operand: one 32-bit LDS base address per (16-idx block u,
+// k-half h) and lane; the buffer / half-tile / k-step offset is the instruction's immediate, so
+// the whole main loop addresses LDS with NU x 2 base registers.
 template <int NU>  // NU 16-idx blocks per quadrant
 struct G8ColRd {
-  uint32_t off[NU][2];
-  __device__ __forceinline__ void init(int lane, int u0) {
+  uint32_t base[NU][2];
+  __device__ __forceinline__ void init(uint32_t region, int lane, int u0) {
     const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -206,13 +213,14 @@ struct G8ColRd {
       for (int h = 0; h < 2; ++h) {
         const int kr = 8 * G + q + 4 * h;
         const int chunk = 2 * (u0 + u) + (p >> 1);
-        off[u][h] = kr * 256 + ((chunk ^ colswz(kr)) << 4) + (p & 1) * 8;
+        base[u][h] = region + kr * 256 + ((chunk ^ colswz(kr)) << 4) + (p & 1) * 8;
       }
   }
-  // half: LDS byte address (32-bit) of the half-tile
-  __device__ __forceinline__ bf16x8_t frag(uint32_t half, int u, int s) const {
-    const s16x4_t lo = g8_tr_read(half + s * 32 * 256 + off[u][0]);
-    const s16x4_t hi = g8_tr_read(half + s * 32 * 256 + off[u][1]);
+  // HALF: byte offset of the half-tile inside the operand's LDS region; S: k-step (32 k-rows)
+  template <int HALF, int S>
+  __device__ __forceinline__ bf16x8_t frag(int u) const {
+    const s16x4_t lo = g8_tr_read<HALF + S * 32 * 256>(base[u][0]);
+    const s16x4_t hi = g8_tr_read<HALF + S * 32 * 256>(base[u][1]);
     const g8_s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8_t, v);
   }
@@ -262,8 +270,10 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   else opB.init(B, p.ldb, n0, 0, kbeg, kend, tid);
 
   // LDS byte offsets: buffer q, A half a / B half b
-  auto a_half = [&](int q, int a) { return q * C::BUF + a * C::HBYTES_A; };
-  auto b_half = [&](int q, int bh) { return q * C::BUF + 2 * C::HBYTES_A + bh * C::HBYTES_B; };
+  // LDS: A region [buffer 0 half 0 | b0 h1 | b1 h0 | b1 h1], then the B region the same way
+  // (every half-tile of one operand within 64 KiB of its region base: 16-bit ds offsets)
+  auto a_half = [&](int q, int a) { return (2 * q + a) * C::HBYTES_A; };
+  auto b_half = [&](int q, int bh) { return 4 * C::HBYTES_A + (2 * q + bh) * C::HBYTES_B; };
 
   const uint32_t lds32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   // read-side lane offsets
@@ -271,8 +281,8 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   rowrd.init(lane);
   G8ColRd<TI> colA;
   G8ColRd<TJ> colB;
-  if constexpr (ACOL) colA.init(lane, wr * QM / 16);
-  if constexpr (BCOL) colB.init(lane, wc * QN / 16);
+  if constexpr (ACOL) colA.init(lds32, lane, wr * QM / 16);
+  if constexpr (BCOL) colB.init(lds32 + 4 * C::HBYTES_A, lane, wc * QN / 16);
 
   f32x4_t acc[2][2][TI][TJ];
 #pragma unroll
@@ -286,25 +296,35 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
 
   bf16x8_t fa[TI][2], fb0[TJ][2], fb1[TJ][2];
 
-  auto readA = [&](int q, int a) {
-    const char* hp = smem + a_half(q, a);
+  auto readA = [&](auto qc, auto ac) {
+    constexpr int q = decltype(qc)::value, a = decltype(ac)::value;
+    constexpr int OFF = (2 * q + a) * C::HBYTES_A;  // = a_half(q, a)
+    const char* hp = smem + OFF;
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if constexpr (!ACOL) fa[i][s] = rowrd.frag(hp, wr * QM + 16 * i, s);
-        else fa[i][s] = colA.frag(lds32 + a_half(q, a), i, s);
+    for (int i = 0; i < TI; ++i) {
+      if constexpr (!ACOL) {
+        fa[i][0] = rowrd.frag(hp, wr * QM + 16 * i, 0);
+        fa[i][1] = rowrd.frag(hp, wr * QM + 16 * i, 1);
+      } else {
+        fa[i][0] = colA.template frag<OFF, 0>(i);
+        fa[i][1] = colA.template frag<OFF, 1>(i);
       }
+    }
   };
-  auto readB = [&](int q, int bh, bf16x8_t (&fb)[TJ][2]) {
-    const char* hp = smem + b_half(q, bh);
+  auto readB = [&](auto qc, auto bc, bf16x8_t (&fb)[TJ][2]) {
+    constexpr int q = decltype(qc)::value, bh = decltype(bc)::value;
+    constexpr int OFF = (2 * q + bh) * C::HBYTES_B;  // offset inside the B region
+    const char* hp = smem + 4 * C::HBYTES_A + OFF;
 #pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if constexpr (!BCOL) fb[j][s] = rowrd.frag(hp, wc * QN + 16 * j, s);
-        else fb[j][s] = colB.frag(lds32 + b_half(q, bh), j, s);
+    for (int j = 0; j < TJ; ++j) {
+      if constexpr (!BCOL) {
+        fb[j][0] = rowrd.frag(hp, wc * QN + 16 * j, 0);
+        fb[j][1] = rowrd.frag(hp, wc * QN + 16 * j, 1);
+      } else {
+        fb[j][0] = colB.template frag<OFF, 0>(j);
+        fb[j][1] = colB.template frag<OFF, 1>(j);
       }
+    }
   };
   auto mma = [&](int a, int bh, const bf16x8_t (&fb)[TJ][2]) {
     __builtin_amdgcn_s_setprio(1);
@@ -345,11 +365,15 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   if (wr == 1) G8_BAR();  // stagger: the second wave row runs one barrier behind
 
   // one K-tile in buffer Q: 4 phases. `full`: issue the DMAs of the K-tiles two ahead.
-  auto ktile = [&](const int Q, int t, bool full) {
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto ktile = [&](auto Qc, int t, bool full) {
+    constexpr int Q = decltype(Qc)::value;
+    using IQ = std::integral_constant<int, Q>;
     // phase 1: B_lo -> fb0, A_lo -> fa; DMA A_hi of the other buffer (K-tile t + 1)
-    readB(Q, 0, fb0);
+    readB(IQ{}, I0{}, fb0);
     __builtin_amdgcn_sched_barrier(0);
-    readA(Q, 0);
+    readA(IQ{}, I0{});
     if (Q == 0 || full) dmaA(1 - Q, 1, t + 1);
     lgk_wait<C::RA>();  // B_lo reads retired before the barrier (B_lo is re-staged in phase 2)
     G8_BAR();
@@ -357,14 +381,14 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     mma(0, 0, fb0);
     G8_BAR();
     // phase 2: B_hi -> fb1; DMA B_lo (K-tile t + 2)
-    readB(Q, 1, fb1);
+    readB(IQ{}, I1{}, fb1);
     if (full) dmaB(Q, 0, t + 2);
     G8_BAR();
     landed(fb1, false);
     mma(0, 1, fb1);
     G8_BAR();
     // phase 3: A_hi -> fa; DMA A_lo (t + 2)
-    readA(Q, 1);
+    readA(IQ{}, I1{});
     if (full) dmaA(Q, 0, t + 2);
     G8_BAR();
     landed(fb1, true);
@@ -384,12 +408,12 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
 
   const int iters = nt >> 1;
   for (int it = 0; it < iters - 1; ++it) {
-    ktile(0, 2 * it, true);
-    ktile(1, 2 * it + 1, true);
+    ktile(I0{}, 2 * it, true);
+    ktile(I1{}, 2 * it + 1, true);
   }
   // last pair: the even tile's phase 1 still issues the odd tile's A_hi; no further DMA
-  ktile(0, nt - 2, false);
-  ktile(1, nt - 1, false);
+  ktile(I0{}, nt - 2, false);
+  ktile(I1{}, nt - 1, false);
   if (wr == 0) G8_BAR();  // close the stagger
   lgk_wait<0>();
   __syncthreads();
@@ -487,7 +511,92 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
   return 0;
 }
 
+// bias gradient partials of the weight-gradient path: bpart[b, n] = sum of G[m, n] over the
+// CS rows of row block b (fp32). A workgroup covers 256 columns x CS rows: 32 column groups of 8
+// (16-byte loads) x 8 row lanes, CS / 8 independent loads in flight per thread, the 8 row lanes
+// reduced through LDS. The deterministic reduce kernel sums the row blocks.
+constexpr int CS_ROWS = 128;
+__global__ __launch_bounds__(256) void g8_colsum_kernel(const bf16_t* __restrict__ G, int64_t ldg,
+                                                        int M, int N, float* __restrict__ bpart) {
+  __shared__ float red[8][256 + 4];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int n8 = blockIdx.x * 256 + cg * 8;
+  const int m0 = blockIdx.y * CS_ROWS;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n8 < N) {
+#pragma unroll 4
+    for (int r = rl; r < CS_ROWS; r += 8) {
+      const int m = m0 + r;
+      if (m < M) {
+        float v[8];
+        Vec8<bf16_t>::load(G + (int64_t)m * ldg + n8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cg * 8 + e] = acc[e];
+  __syncthreads();
+  const int col = threadIdx.x;  // 256 columns of this block, one per thread
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t += red[k][col];
+  const int n = blockIdx.x * 256 + col;
+  if (n < N) bpart[(int64_t)blockIdx.y * N + n] = t;
+}
+
 }  // namespace
+
+// Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
+// B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers
+// about half the chip (the other half stays free for the dgrad / attention kernels running
+// concurrently on the compute stream or other client lanes); fp32 slice partials are summed by
+// the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials.
+int wgrad_g8_splits(int M, int N, int K, int* Mc) {
+  if (N % BN8 || K % BN8 || N <= 0 || M <= 0) return 0;
+  static const int slots = [] {
+    const char* e = std::getenv("BCFL_G8_WGRAD_SLOTS");
+    const int v = e ? std::atoi(e) : 128;
+    return v > 0 ? v : 128;
+  }();
+  const int tiles = (N / BN8) * (K / BN8);  // 256 x 256 output tiles of dW[N, K]
+  int S = (slots + tiles - 1) / tiles;
+  const int maxS = M / 1024 > 0 ? M / 1024 : 1;  // keep >= 16 K-tiles per slice
+  if (S > maxS) S = maxS;
+  if (S < 1) S = 1;
+  int mc = (M + S - 1) / S;
+  mc = (mc + 127) / 128 * 128;
+  *Mc = mc;
+  return (M + mc - 1) / mc;
+}
+
+int launch_wgrad_g8(const WgradParams& p, hipStream_t s) {
+  if (p.N % BN8 || p.K % BN8 || p.S < 1 || (p.S > 1 && !p.part)) return -1;
+  G8Params g{p.G, p.X, p.S > 1 ? nullptr : p.out, p.ldg, p.ldx, p.S > 1 ? (int64_t)p.K : p.ldo,
+             p.N, p.K, p.M};
+  g.a_col = 1;
+  g.b_col = 1;
+  g.bm = 256;
+  g.splits = p.S;
+  g.kc = p.Mc;
+  g.epi = p.S > 1 ? EPI_PARTIAL : EPI_STORE;
+  g.part = p.part;
+  int rc = launch_g8(g, s);
+  if (rc) return rc;
+  const int SB = wgrad_g8_bias_parts(p.M);
+  if (p.dbias) {
+    const dim3 cg((p.N + 255) / 256, SB);
+    hipLaunchKernelGGL(g8_colsum_kernel, cg, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(p.G),
+                       p.ldg, p.M, p.N, p.dbias_part);
+  }
+  if (p.S > 1 || p.dbias)
+    return launch_wgrad_reduce(p.S > 1 ? p.part : nullptr, p.S, p.N, p.K, p.out, p.ldo,
+                               p.dbias ? p.dbias_part : nullptr, p.dbias, s, SB);
+  return 0;
+}
+
+int wgrad_g8_bias_parts(int M) { return (M + CS_ROWS - 1) / CS_ROWS; }
 
 // Block-row choice: a launch takes ceil(tiles / 256 CUs) waves of tiles, a 128-row tile takes
 // ~0.57 of a 256-row tile's time (measured 1.15x less efficient per FLOP). Pick the smaller

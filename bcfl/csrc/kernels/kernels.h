@@ -97,6 +97,14 @@ struct WgradParams {
 // number of splits S and rows per split Mc for an M x N x K weight gradient (-1: unsupported)
 int wgrad_splits(int M, int N, int K, int* Mc);
 int launch_wgrad(const WgradParams& p, hipStream_t s);
+// out[n, k] = bf16(sum_s part[s, n, k]); with bpart: dbias[n] = bf16(sum_s bpart[s, n])
+int launch_wgrad_reduce(const float* part, int S, int N, int K, void* out, int64_t ldo,
+                        const float* bpart, void* dbias, hipStream_t s, int SB = 0);
+int wgrad_g8_bias_parts(int M);  // rows of the bias-partial buffer the g8 weight gradient needs
+// weight gradient on the 8-phase kernel (gemm8.hip, both operands transposed-read): split count
+// for an M x N x K problem (0 = shape not supported) and the launch (p.S / p.Mc from it)
+int wgrad_g8_splits(int M, int N, int K, int* Mc);
+int launch_wgrad_g8(const WgradParams& p, hipStream_t s);
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
 enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3, EPI_ACCUM = 4,

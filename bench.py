@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
     ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
+    ap.add_argument("--anomaly-filter", default=None,
+                    help="override the preset's update anomaly filter (none|pagerank|modz|both)")
     ap.add_argument("--no-info-passing", action="store_true",
                     help="skip the post-run information-passing measurement (N > 1)")
     ap.add_argument("--global-test-samples", type=int, default=0,
@@ -115,7 +117,8 @@ def main():
                      device=a.device, client_lanes=a.lanes, micro_batches=a.micro_batches,
                      overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad),
                      **({"global_test_samples": a.global_test_samples}
-                        if a.global_test_samples > 0 else {}))
+                        if a.global_test_samples > 0 else {}),
+                     **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}))
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
         fed.run_round(r)

@@ -1,0 +1,94 @@
+#!/usr/bin/env python
+"""The reference's worker grid on MI355X: server (FedAvg) vs serverless (P2P gossip) at 5 / 10 /
+20 clients, 20 rounds each — the experiment behind the latency and accuracy bar charts of
+``All_graphs_IMDB_dataset.ipynb:747-748`` (latency) and ``:830-831`` (accuracy).
+
+Setup (both modes identical except the protocol): IMDB-shaped synthetic data, IID, 100 train /
+100 test rows per client (``server_IID_IMDB.py:79-84`` / ``serverless_IID_IMDB.py:258``),
+BERT-base (the BioBERT architecture of the server script), random init with the learnable
+protocol of ``baseline3_learnable``, class-balanced 1000-row global draw, all clients on one GPU
+(client lanes), per-round checkpoints and the ledger on.
+
+    python benchmarks/worker_grid.py [--clients 5 10 20] [--rounds 20] [--out profiles/x.json]
+"""
+from __future__ import annotations
+
+import argparse
+import gc
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt: bool) -> dict:
+    import torch
+    from bcfl.config import get_preset
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    t_proc = time.time()
+    part = "shared_random" if mode == "server" else "iid_random"
+    cfg = get_preset("baseline3_learnable", mode=mode, model=model, num_clients=clients,
+                     num_rounds=rounds, partition=part, train_samples=100, test_samples=100,
+                     resample_each_round=(mode == "serverless"), out_dir=out_dir,
+                     reference_prints=False, save_every=1, keep_optimizer_state=keep_opt)
+    fed = Federation(cfg, verbose=False)
+    times = []
+    for r in range(rounds):
+        t0 = time.perf_counter()
+        fed.run_round(r)
+        if fed.is_cuda:
+            torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    fed.drain()
+    fa = fed.federation_accuracy()
+    fed.finish()
+    steady = times[3:] if len(times) > 4 else times
+    rec = {"mode": mode, "clients": clients, "rounds": rounds, "model": model,
+           "keep_optimizer_state": keep_opt,
+           "s_per_round_steady": sum(steady) / len(steady), "total_rounds_s": sum(times),
+           "process_latency_min": (time.time() - t_proc) / 60.0,
+           "final_accuracy": fa.get("accuracy"), "global_eval_rows": fa.get("rows"),
+           "final_majority_rate": fed.history[-1].get("global_majority_rate"),
+           "accuracy_curve": list(fed.global_accuracies), "lanes": len(fed.lanes) or 1,
+           "hbm_peak_gb": fed.history[-1].get("hbm_peak_gb")}
+    del fed
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+    return rec
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, nargs="+", default=[5, 10, 20])
+    ap.add_argument("--modes", nargs="+", default=["server", "serverless"])
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--model", default="bert-base")
+    ap.add_argument("--out", default="gpurun_out/worker_grid.json")
+    ap.add_argument("--fresh-adamw", action="store_true",
+                    help="the reference's fresh AdamW per round (oscillates on IID from random "
+                         "init, profiles/accuracy_server_stability.json); default keeps moments")
+    a = ap.parse_args(argv)
+    res = {"reference": {"latency_min_server": [38, 41.8, 45.4], "latency_min_serverless": [27.8, 40, 41.5],
+                         "acc_server": [68, 74, 80], "acc_serverless": [76, 83, 88],
+                         "source": "All_graphs_IMDB_dataset.ipynb:747-748,830-831 (5/10/20 workers, 20 rounds, hardware unspecified, pretrained models)"},
+           "runs": []}
+    for k in a.clients:
+        for mode in a.modes:
+            rec = one(mode, k, a.rounds, os.path.join("runs", "grid", f"{mode}{k}"), a.model,
+                      not a.fresh_adamw)
+            print(json.dumps({x: rec[x] for x in rec if x != "accuracy_curve"}), flush=True)
+            res["runs"].append(rec)
+            os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+            with open(a.out, "w") as fh:
+                json.dump(res, fh, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -79,6 +79,71 @@ def check(dev):
     return res
 
 
+def check_wgrad(dev):
+    import os
+    C = native()
+    res = []
+    for M, N, K in [(7680, 768, 768), (7777, 2304, 768), (1500, 768, 3072), (11264, 3072, 768)]:
+        g = torch.Generator(device=dev).manual_seed(M + N)
+        G = (torch.rand(M, N, generator=g, device=dev) * 2 - 1).bfloat16()
+        X = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).bfloat16()
+        ref = G.float().t() @ X.float()
+        rb = G.float().sum(0)
+        os.environ["BCFL_WGRAD_G8"] = "1"
+        dw, db = C.wgrad_bias(G, X)
+        torch.cuda.synchronize()
+        e = ((dw.float() - ref).norm() / ref.norm()).item()
+        eb = ((db.float() - rb).norm() / rb.norm()).item()
+        r = {"wgrad": [M, N, K], "rel": e, "bias_rel": eb, "ok": e < 1e-2 and eb < 1e-2}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    return res
+
+
+def bench_wgrad(dev, reps):
+    import os
+    C = native()
+    out = []
+    for name, M, N, K in [("qkv_wgrad", 7680, 2304, 768), ("attn_out_wgrad", 7680, 768, 768),
+                          ("ffn_up_wgrad", 7680, 3072, 768), ("ffn_down_wgrad", 7680, 768, 3072),
+                          ("ffn_up_wgrad_11k", 11264, 3072, 768)]:
+        g = torch.Generator(device=dev).manual_seed(2)
+        G = (torch.rand(M, N, generator=g, device=dev) * 2 - 1).bfloat16()
+        X = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).bfloat16()
+
+        def k9():
+            os.environ["BCFL_WGRAD_G8"] = "0"
+            return C.wgrad_bias(G, X)
+
+        def g8():
+            os.environ["BCFL_WGRAD_G8"] = "1"
+            return C.wgrad_bias(G, X)
+        arms = {"hipblaslt": lambda: (G.t() @ X, G.sum(0)), "k9": k9, "g8": g8}
+        for f in arms.values():
+            f()
+        torch.cuda.synchronize()
+        times = {k: [] for k in arms}
+        for _ in range(reps):
+            for k, f in arms.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    f()
+                e1.record()
+                e1.synchronize()
+                times[k].append(e0.elapsed_time(e1) / 5)
+        fl = 2.0 * M * N * K
+        rec = {"shape": name, "M": M, "N": N, "K": K}
+        for k, ts in times.items():
+            ts.sort()
+            rec[k + "_us"] = round(ts[len(ts) // 2] * 1000, 1)
+            rec[k + "_tflops"] = round(fl / (ts[len(ts) // 2] * 1e-3) / 1e12, 1)
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+    os.environ["BCFL_WGRAD_G8"] = "1"
+    return out
+
+
 def bench(dev, reps):
     C = native()
     shapes = [  # name, M, N, K, kind ('fwd' = x W^T, 'dgrad' = g W)
@@ -138,16 +203,19 @@ def bench(dev, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--wgrad-only", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default="gpurun_out/g8.json")
     a = ap.parse_args()
     dev = torch.device("cuda")
     t0 = time.time()
-    res = {"check": check(dev)}
-    ok = all(r["ok"] and r["epi_ok"] for r in res["check"])
+    res = {"check": check(dev), "check_wgrad": check_wgrad(dev)}
+    ok = all(r["ok"] and r["epi_ok"] for r in res["check"]) and all(r["ok"] for r in res["check_wgrad"])
     print("CHECK", "PASS" if ok else "FAIL", flush=True)
     if ok and not a.check_only:
-        res["bench"] = bench(dev, a.reps)
+        res["bench_wgrad"] = bench_wgrad(dev, a.reps)
+        if not a.wgrad_only:
+            res["bench"] = bench(dev, a.reps)
     res["wall_s"] = time.time() - t0
     import os
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
