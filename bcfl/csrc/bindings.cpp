@@ -130,9 +130,20 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, Tensor y, optional<Tensor> bias, i
 }
 
 // ------------------------------------------------------------------------------------------------
+// optional work order (bcfl.data.batching.attn_schedule): [2, n] int32 on the device, row 0 the
+// query-block order (forward, dQ), row 1 the key-block order (dK / dV)
+static void attn_sched_check(const c10::optional<Tensor>& sched) {
+  if (!sched.has_value() || !sched->defined()) return;
+  check_cuda(*sched, "attention schedule");
+  TORCH_CHECK(sched->scalar_type() == at::kInt && sched->dim() == 2 && sched->size(0) == 2 &&
+                  sched->is_contiguous(),
+              "attention schedule must be a contiguous [2, n] int32 tensor");
+}
+
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor cu, int64_t max_s, int64_t nh, int64_t nkv,
                              int64_t d, double scale, bool causal, int64_t p8, int64_t ka,
-                             int64_t kb) {
+                             int64_t kb, c10::optional<Tensor> sched) {
+  attn_sched_check(sched);
   check_cuda(qkv, "qkv");
   check_cuda(cu, "cu_seqlens");
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16, "attention kernels take bf16");
@@ -161,13 +172,18 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor cu, int64_t max_s, int64_t nh, i
     p.mask = reinterpret_cast<uint32_t*>(mask.data_ptr<int>());
     p.mask_w = W;
   }
+  if (sched.has_value() && sched->defined() && sched->size(1) > 0) {
+    p.sched = sched->data_ptr<int>();
+    p.n_units = (int)sched->size(1);
+  }
   if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_fwd(p, stream()), "attn_fwd");
   return {out, lse, mask};
 }
 
 Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int64_t max_s,
                 int64_t nh, int64_t nkv, int64_t d, double scale, bool causal, int64_t p8,
-                int64_t ka, int64_t kb, Tensor mask) {
+                int64_t ka, int64_t kb, Tensor mask, c10::optional<Tensor> sched) {
+  attn_sched_check(sched);
   check_cuda(dout, "dout");
   check_cuda(qkv, "qkv");
   check_cuda(out, "out");
@@ -195,6 +211,11 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
                 "attn_bwd: dropout keep bitmask from attn_fwd required");
     p.mask = reinterpret_cast<const uint32_t*>(mask.data_ptr<int>());
     p.mask_w = W;
+  }
+  if (sched.has_value() && sched->defined() && sched->size(1) > 0) {
+    p.sched_q = sched->data_ptr<int>();
+    p.sched_k = p.sched_q + sched->size(1);
+    p.n_units = (int)sched->size(1);
   }
   if (T > 0 && p.B > 0) check_rc(bcfl::launch_attn_bwd(p, stream()), "attn_bwd");
   return dqkv;
@@ -795,8 +816,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_dgrad_acc", &linear_dgrad_acc);
   m.def("linear_fwd_acc", &linear_fwd_acc);
   m.def("gemm_native_ok", &gemm_native_ok);
-  m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("cu"), py::arg("max_s"), py::arg("nh"),
+        py::arg("nkv"), py::arg("d"), py::arg("scale"), py::arg("causal"), py::arg("p8"),
+        py::arg("ka"), py::arg("kb"), py::arg("sched") = py::none());
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"),
+        py::arg("cu"), py::arg("max_s"), py::arg("nh"), py::arg("nkv"), py::arg("d"),
+        py::arg("scale"), py::arg("causal"), py::arg("p8"), py::arg("ka"), py::arg("kb"),
+        py::arg("mask"), py::arg("sched") = py::none());
   m.def("emb_ln_fwd", &emb_ln_fwd);
   m.def("emb_ln_bwd", &emb_ln_bwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);

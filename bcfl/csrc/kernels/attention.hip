@@ -38,9 +38,11 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
+#include "lds_dma.h"
 #include "mfma_tiles.h"
 
 namespace bcfl {
@@ -53,6 +55,10 @@ constexpr int TILE = 64;              // inner tile
 constexpr int DROP_STRIDE = 8192;     // dropout element index = (tq*nh + h)*8192 + key_pos
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
+// forward: the running row max m is only raised (O and l rescaled) when a tile's max exceeds it
+// by more than this (log2 units): P <= 2^8 then, harmless for bf16 P and fp32 sums, and the rescale
+// leaves the tile loop after the first tile or two
+constexpr float RESCALE_LOG2 = 8.f;
 
 // raw v_exp_f32: softmax arguments are <= 0 and a flushed denormal result is harmless, so skip
 // exp2f's denormal range-reduction (cmp + 2 cndmask + add + ldexp per element).
@@ -104,33 +110,122 @@ struct Stage2 {
 };
 
 // ------------------------------------------------------------------------------------------------
-// WPE: minimum waves per SIMD the register allocation must allow (1 = unconstrained: 224
-// registers, 2 waves/SIMD; 3 = 168 registers with a few spilled to scratch). Picked per launch
-// (attn_occupancy(): BCFL_ATTN_WPE, default below) so both variants can be A/B-timed in one process.
-template <int HD, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_kernel(AttnParams p) {
-  constexpr int STG = 2 * TILE * HD;  // K tile | V tile
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);  // [2 stages][K tile | V tile]
+// Work order. A launch is (head, unit) with unit = (sequence b, 128-row block); with a schedule
+// (attn_schedule, built on the host with the batch) units come longest-sequence first, so the
+// dispatcher starts the long blocks at once and back-fills with short ones (LPT order). Without
+// one, every (b, block < ceil(max_s / 128)) in batch order.
+__device__ __forceinline__ void attn_unit(const int* sched, int u, int max_s, int& b, int& blk) {
+  if (sched) {
+    const int e = sched[u];
+    b = e >> 12;
+    blk = e & 4095;
+  } else {
+    const int nb = (max_s + BLK - 1) / BLK;
+    b = u / nb;
+    blk = u - b * nb;
+  }
+}
 
-  const int b = blockIdx.z, h = blockIdx.y;
+// the partner half-wave's value (lane l ^ 32) as v_permlane32_swap: returns {lo-half image,
+// hi-half image}; max / sum of a lane and its partner is op(r[0], r[1]) on every lane
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ uint32_t xor32_get(uint32_t x, int hh) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return hh ? r[0] : r[1];
+}
+
+// bit of key j (0..31 inside its 32-key block) in a keep word (kernels.h)
+__device__ __forceinline__ int attn_mbit(int j) { return 8 * (j & 3) + ((j >> 3) & 3) + 4 * ((j >> 2) & 1); }
+
+// keep flags of 4 scores from one 32-bit hash (byte e decides score e): bit 7 of byte e of the
+// result is set iff byte e >= p8. SWAR: (x | 0x80) - p7 keeps each byte >= 1 (no borrow across
+// bytes) and has bit 7 set iff (x & 0x7f) >= p7; combined with x's own bit 7 by OR (p8 < 128)
+// or AND (p8 >= 128).
+template <int DROP>  // 1: p8 < 128, 2: p8 >= 128
+__device__ __forceinline__ uint32_t keep_flags4(uint32_t x, uint32_t p7x4) {
+  const uint32_t t = (x | 0x80808080u) - p7x4;
+  return DROP == 2 ? (x & t) : (x | t);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward. K / V tiles arrive by LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave
+// instruction, rows past the sequence end zero-filled by the buffer range check) into a 2-deep
+// ring: tile i + 1 is in flight while tile i is computed, with one counted wait and one barrier
+// per tile and no VGPR staging. Per tile and wave (32 queries x 64 keys, 32 scores per lane):
+//   * S^T = K Q^T on MFMA (8 x 32x32x16), the query on the lane;
+//   * p = exp2(s * scale * log2e - m); the running max m is raised (with the O / l rescale) only
+//     when a tile's max exceeds it by RESCALE_LOG2 — in practice on the first tile only;
+//   * dropout: one 32-bit hash per 4 scores; the 4 keep decisions are made at once (SWAR byte
+//     compare, keep_flags4), expanded by two v_perm_b32 into bf16-pair masks ANDed into the
+//     packed P, and folded into the keep bitmask with one bit-field insert;
+//   * keep words are staged in LDS (a 16-word ring per query) and flushed with coalesced stores
+//     every 8 tiles and at the end — no stores inside the tile loop;
+//   * O += P V on MFMA with the accumulator as the B operand, V read by ds_read_b64_tr_b16 (asm,
+//     immediate offsets: the compiler would drain the DMA queue before the builtin form).
+template <int HD>
+struct FwdCfg {
+  static constexpr int CPR = HD / 8;              // 16-B chunks per K / V row
+  static constexpr int TBYTES = TILE * HD * 2;    // one K or V tile
+  static constexpr int PW = TBYTES / 1024 / NWAVE;  // DMA pieces per wave per tensor
+  static constexpr int STG = 2 * TBYTES;          // K | V
+  static constexpr int MW = 16;                   // keep words staged per query (8 tiles)
+  static constexpr int MWS = 20;                  // padded LDS row (16-B aligned, 2-way writes)
+  static constexpr int LDS = 2 * STG + NWAVE * ROWS * MWS * 4;
+  static_assert(PW >= 1, "tile geometry");
+};
+
+template <int HD, int WPE, int DROP>  // DROP: 0 none, 1 p8 < 128, 2 p8 >= 128
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_kernel(AttnParams p) {
+  using C = FwdCfg<HD>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int b, qb;
+  attn_unit(p.sched, blockIdx.y, p.max_s, b, qb);
+  const int h = blockIdx.x;
   const int tok0 = p.cu[b];
   const int L = p.cu[b + 1] - tok0;
-  const int q0 = blockIdx.x * BLK;
+  const int q0 = qb * BLK;
   if (q0 >= L) return;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qw0 = q0 + wid * ROWS;
   const bool active = qw0 < L;
   const int hk = h / (p.nh / p.nkv);
   const int rs = (p.nh + 2 * p.nkv) * HD;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
-  const bf16_t* ksrc = qkv + p.nh * HD + hk * HD;
-  const bf16_t* vsrc = qkv + (p.nh + p.nkv) * HD + hk * HD;
   const int kend = p.causal ? min(L, q0 + BLK) : L;
   const int ntiles = (kend + TILE - 1) / TILE;
 
-  Stage2<HD> stg;
-  stg.load(ksrc, rs, vsrc, rs, tok0, 0, L);
+  // ---- K / V tile DMA: one resource over this sequence's rows --------------------------------
+  const __amdgpu_buffer_rsrc_t rsrc = buf_rsrc(qkv, (int64_t)tok0 * rs * 2, (int64_t)L * rs * 2);
+  int voff[2][C::PW];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int colbase = (x == 0 ? p.nh + hk : p.nh + p.nkv + hk) * HD;
+#pragma unroll
+    for (int i = 0; i < C::PW; ++i) {
+      const int c = 64 * (wid + NWAVE * i) + lane;  // LDS chunk of the tile this lane fills
+      const int row = c / C::CPR;
+      const int u = (c % C::CPR) ^ swz<HD>(row);    // source chunk (the swizzle is an involution)
+      voff[x][i] = row * rs * 2 + (colbase + 8 * u) * 2;
+    }
+  }
+  auto dma = [&](int st, int k0) {
+    const int ko = k0 * rs * 2;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < C::PW; ++i)
+        dma16(rsrc, smem + st * C::STG + x * C::TBYTES + (wid + NWAVE * i) * 1024, voff[x][i] + ko);
+  };
+  dma(0, 0);
 
   bf16x8_t qf[HD / 16];
   {
@@ -142,51 +237,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   f32x16_t o[HD / 32];
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) o[u] = zero16();
-  float m = -INFINITY, l = 0.f;  // m: running max in the scaled log2 domain
+  float m = 0.f, l = 0.f;  // m: row max of the first tile in the scaled log2 domain
   const float sl2 = p.scale * LOG2E;
-  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
+  const float sd = DROP ? keep_scale(p.p8) : 1.f;
   const int myq = qw0 + r;
-  const uint32_t drow = (uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE;
-  // this lane's keep-bit row (query clamped into the sequence: rows past L are never read)
-  uint32_t* mrow = p.mask + (size_t)((tok0 + min(myq, L - 1)) * p.nh + h) * p.mask_w;
+  const uint32_t cnt0 = ((uint32_t)((tok0 + myq) * p.nh + h) * (uint32_t)DROP_STRIDE + 4u * hh) >> 2;
+  const uint32_t p7x4 = (p.p8 & 0x7fu) * 0x01010101u;
+
+  // keep-word staging: this wave's [32 queries][MWS] words
+  uint32_t* mst = reinterpret_cast<uint32_t*>(smem + 2 * C::STG) + wid * ROWS * C::MWS;
+  int mflushed = 0;  // first keep word not yet flushed (multiple of MW)
+  auto flush = [&](int wend) {  // words [mflushed, wend) of the wave's rows -> global
+    const int row = lane >> 1, half = lane & 1;
+    const int q = qw0 + row;
+    if (q < L) {
+      uint32_t* g = p.mask + (size_t)((tok0 + q) * p.nh + h) * p.mask_w + mflushed;
+      const uint32_t* sp = mst + row * C::MWS;
+#pragma unroll
+      for (int i = 0; i < C::MW / 2; ++i) {
+        const int wdx = (C::MW / 2) * half + i;
+        if (mflushed + wdx < wend) g[wdx] = sp[wdx];
+      }
+    }
+    mflushed = wend;
+  };
 
   TileOffsets<HD> to;
   to.init(lane);
-  stg.store(lds, lds + TILE * HD);
-  __syncthreads();
+  const uint32_t lds32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  uint32_t rowb[HD / 16];    // row-read bases (K tile of stage 0)
+#pragma unroll
+  for (int s2 = 0; s2 < HD / 16; ++s2) rowb[s2] = lds32 + 2 * to.row[s2];
+  uint32_t trb[HD / 32][2];  // transposed-read bases (V tile of stage 0)
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) trb[u][hi] = lds32 + C::TBYTES + 2 * to.tr[u][hi];
 
-  for (int it = 0; it < ntiles; ++it) {
+  vm_wait<0>();
+  // Q has landed: tell the compiler (its waitcnt pass would otherwise keep treating the Q loads
+  // as outstanding inside the loop and count the in-flight DMAs down before every Q MFMA)
+#pragma unroll
+  for (int s2 = 0; s2 < HD / 16; ++s2) reg_fence(qf[s2]);
+  BCFL_BAR();
+
+  auto tile = [&](auto stc, int it) {
+    constexpr int ST = decltype(stc)::value;
     const int k0 = it * TILE;
-    const bool more = it + 1 < ntiles;
-    if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);  // in flight during the MFMAs
-    const bf16_t* Ks = lds + (it & 1) * STG;
-    const bf16_t* Vs = Ks + TILE * HD;
-    if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
-      f32x16_t sacc[2];
+    if (it > 0) {
+      vm_wait<0>();  // this wave's pieces of tile it have landed ...
+      BCFL_BAR();    // ... and every wave's; every wave is done with tile it - 1's buffer
+    }
+    if (it + 1 < ntiles) dma(ST ^ 1, k0 + TILE);
+    if (!active || (p.causal && k0 > qw0 + ROWS - 1)) return;
+    // S^T = K Q^T: K fragments by asm row reads (immediate offsets), half t = 0 consumed while
+    // half 1 is still in flight
+    bf16x8_t kf[2][HD / 16];
+    auto kread = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int OFF = ST * C::STG + 32 * t * HD * 2;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        sacc[t] = zero16();
+      for (int s = 0; s < HD / 16; ++s) kf[t][s] = ds_row_read<OFF>(rowb[s]);
+    };
+    kread(std::integral_constant<int, 0>{});
+    kread(std::integral_constant<int, 1>{});
+    f32x16_t sacc[2];
+    lgk_wait<HD / 16>();
 #pragma unroll
-        for (int s = 0; s < HD / 16; ++s)
-          sacc[t] = mfma32(lds_row8(Ks + 32 * t * HD + to.row[s]), qf[s], sacc[t]);
-      }
-      const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
-      if (need_mask) {
+    for (int s = 0; s < HD / 16; ++s) reg_fence(kf[0][s]);
+    sacc[0] = zero16();
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+    for (int s = 0; s < HD / 16; ++s) sacc[0] = mfma32(kf[0][s], qf[s], sacc[0]);
+    lgk_wait<0>();
 #pragma unroll
-          for (int reg = 0; reg < 16; ++reg) {
-            const int key = k0 + 32 * t + acc_row(reg, hh);
-            if (key >= L || (p.causal && key > myq)) sacc[t][reg] = -INFINITY;
-          }
-      }
+    for (int s = 0; s < HD / 16; ++s) reg_fence(kf[1][s]);
+    sacc[1] = zero16();
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) sacc[1] = mfma32(kf[1][s], qf[s], sacc[1]);
+    if ((k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int key = k0 + 32 * t + acc_row(reg, hh);
+          if (key >= L || (p.causal && key > myq)) sacc[t][reg] = -INFINITY;
+        }
+    }
+    {
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) mx = fmaxf(mx, sacc[t][reg]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-      if (__any(mx > m)) {  // rescale only when some row's max grew (wave-uniform branch)
+      mx = xor32_max(mx) * sl2;
+      if (it == 0) {
+        m = mx;
+      } else if (__any(mx > m + RESCALE_LOG2)) {  // wave-uniform, rare after the first tile
         const float mn = fmaxf(m, mx);
         const float alpha = fexp2(m - mn);
         l *= alpha;
@@ -196,50 +342,88 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           for (int reg = 0; reg < 16; ++reg) o[u][reg] *= alpha;
         m = mn;
       }
-      bf16x8_t pf[4];
-      float ls = 0.f;
+    }
+    uint32_t pw[4][4];  // P as bf16 pairs: fragment ks = 2t + (g4 >> 1), word 2 (g4 & 1) + e / 2
+    uint32_t bits[2];
+    float ls;
+    {
+      ls = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        // lane-half hh holds keys acc_row(reg, hh) = (reg & 3) + 8 (reg >> 2) + 4 hh of the block
-        uint32_t bits = 0;
+        bits[t] = 0u;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          uint32_t hsh = 0;
-          if (p.p8) hsh = hash32((drow + (uint32_t)(k0 + 32 * t + 8 * g4 + 4 * hh)) >> 2, p.ka, p.kb);
+          float pv[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int reg = 4 * g4 + e;
-            float pv = fexp2(fmaf(sacc[t][reg], sl2, -m));
-            ls += pv;
-            if (p.p8) {
-              const bool keep = ((hsh >> (8 * e)) & 0xffu) >= p.p8;
-              bits |= (keep ? 1u : 0u) << (e + 8 * g4);
-              pv = keep ? pv : 0.f;  // 1/(1-p) applied at the end
-            }
-            pf[2 * t + (reg >> 3)][reg & 7] = (__bf16)pv;
+            pv[e] = fexp2(fmaf(sacc[t][4 * g4 + e], sl2, -m));
+            ls += pv[e];
           }
-        }
-        if (p.p8) {  // publish the 32 decisions of this (query, key block) for the backward
-          bits <<= 4 * hh;
-          bits |= __shfl_xor(bits, 32, 64);
-          if (hh == t && myq < L) mrow[(k0 >> 5) + t] = bits;  // clamped rows alias row L-1
+          uint32_t w0 = pack2bf(pv[0], pv[1]), w1 = pack2bf(pv[2], pv[3]);
+          if constexpr (DROP != 0) {
+            const uint32_t cnt = (cnt0 + (uint32_t)((k0 >> 2) + 8 * t + 2 * g4)) & 0x3fffffffu;  // uint32 wrap of the element index
+            const uint32_t f = keep_flags4<DROP>(hash32(cnt, p.ka, p.kb), p7x4);
+            const uint32_t fs = f << 8;
+            // v_perm_b32 selectors 8..11 replicate bits 15 / 31 of the low and high source
+            // dwords: {fs, f} -> flag 0 = sel 10, flag 1 = sel 8, flag 2 = sel 11, flag 3 = sel 9
+            w0 &= __builtin_amdgcn_perm(fs, f, 0x08080A0Au);
+            w1 &= __builtin_amdgcn_perm(fs, f, 0x09090B0Bu);
+            // flags (bits 7 + 8e) -> bits 8e + g4 of the keep word
+            bits[t] |= (f >> (7 - g4)) & (0x01010101u << g4);
+          }
+          pw[2 * t + (g4 >> 1)][2 * (g4 & 1)] = w0;
+          pw[2 * t + (g4 >> 1)][2 * (g4 & 1) + 1] = w1;
         }
       }
-      l += ls;
-#pragma unroll
-      for (int u = 0; u < HD / 32; ++u)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          o[u] = mfma32(tr_operand(Vs + 16 * ks * HD, to.tr[u][0], to.tr[u][1]), pf[ks], o[u]);
     }
-    if (more) {
-      bf16_t* nk = lds + ((it + 1) & 1) * STG;
-      stg.store(nk, nk + TILE * HD);
+    l += ls;
+    if constexpr (DROP != 0) {  // publish this (query, 2 key blocks)'s decisions: half hh writes block hh
+      const uint32_t mine = bits[hh] << (4 * hh), other = bits[hh ^ 1] << (4 * hh);
+      const uint32_t word = mine | xor32_get(other, hh);
+      mst[r * C::MWS + ((((k0 >> 5) + hh)) & (C::MW - 1))] = word;
     }
-    __syncthreads();
+    // O += P V: V^T fragments by transposed reads of the stage's V tile
+    bf16x8_t vf[HD / 32][4];
+    auto vread = [&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
+      constexpr int OFF = ST * C::STG + 16 * ks * HD * 2;
+#pragma unroll
+      for (int u = 0; u < HD / 32; ++u) {
+        const s16x4_t lo = ds_tr_read<OFF>(trb[u][0]);
+        const s16x4_t hi = ds_tr_read<OFF>(trb[u][1]);
+        vf[u][ks] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    vread(std::integral_constant<int, 0>{});
+    vread(std::integral_constant<int, 1>{});
+    vread(std::integral_constant<int, 2>{});
+    vread(std::integral_constant<int, 3>{});
+    lgk_wait<0>();
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) reg_fence(vf[u][ks]);
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const uint4 w4 = make_uint4(pw[ks][0], pw[ks][1], pw[ks][2], pw[ks][3]);
+        o[u] = mfma32(vf[u][ks], __builtin_bit_cast(bf16x8_t, w4), o[u]);
+      }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  int it = 0;
+  for (; it + 1 < ntiles; it += 2) {
+    tile(I0{}, it);
+    tile(I1{}, it + 1);
+    if (DROP && ((it + 2) & 7) == 0 && it + 2 < ntiles) flush(2 * (it + 2));
   }
+  if (it < ntiles) tile(I0{}, it);
+  if (DROP && active) flush(2 * ntiles);
   if (!active) return;
-  l += __shfl_xor(l, 32, 64);
+  l = xor32_sum(l);
   if (myq >= L) return;
   const float inv = sd / l;
   bf16_t* orow = reinterpret_cast<bf16_t*>(p.out) + (size_t)(tok0 + myq) * p.nh * HD + h * HD;
@@ -286,10 +470,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  int b, qb;
+  attn_unit(p.sched_q, blockIdx.y, p.max_s, b, qb);
+  const int h = blockIdx.x;
   const int tok0 = p.cu[b];
   const int L = p.cu[b + 1] - tok0;
-  const int q0 = blockIdx.x * BLK;
+  const int q0 = qb * BLK;
   if (q0 >= L) return;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int qw0 = q0 + wid * ROWS;
@@ -367,7 +553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (key >= L || (p.causal && key > myq)) pv = 0.f;
           }
           float dp = pacc[t][reg];
-          if (p.p8) dp = keep_and(dp, wk, (reg & 3) + 8 * (reg >> 2));
+          if (p.p8) dp = keep_and(dp, wk, 8 * (reg & 3) + (reg >> 2));  // key 8 (reg >> 2) + 4 hh + (reg & 3)
           dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
         }
       }
@@ -403,10 +589,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
-  const int b = blockIdx.z, hk = blockIdx.y;
+  int b, kb;
+  attn_unit(p.sched_k, blockIdx.y, p.max_s, b, kb);
+  const int hk = blockIdx.x;
   const int tok0 = p.cu[b];
   const int L = p.cu[b + 1] - tok0;
-  const int kb0 = blockIdx.x * BLK;
+  const int kb0 = kb * BLK;
   if (kb0 >= L) return;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int kw0 = kb0 + wid * ROWS;
@@ -419,6 +607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int voff = (p.nh + p.nkv) * HD + hk * HD;
   const int mykey = kw0 + r;
   const int ki = min(mykey, L - 1);
+  const int mbit = attn_mbit(r);  // my key's bit in a keep word
   const int qstart = p.causal ? (kb0 / TILE) * TILE : 0;
   const int nqt = (L - qstart + TILE - 1) / TILE;  // q tiles per head
   const int ntiles = nqt * grp;
@@ -518,7 +707,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (need_mask && (q >= L || (p.causal && mykey > q))) pv = 0.f;
             float pd = pv, dp = pacc[reg];
             if (p.p8) {
-              const int km = __builtin_amdgcn_sbfe((int)mw[e], r, 1);
+              const int km = __builtin_amdgcn_sbfe((int)mw[e], mbit, 1);
               pd = __int_as_float(__float_as_int(pv) & km);
               dp = __int_as_float(__float_as_int(dp) & km);
             }
@@ -566,21 +755,36 @@ const AttnOcc& attn_occupancy() {
   return o;
 }
 
+int attn_units(int n_units, int B, int max_s) {
+  return n_units > 0 ? n_units : B * ((max_s + BLK - 1) / BLK);
+}
+
+template <int HD, int WPE>
+void fwd_launch(const AttnParams& p, dim3 grid, size_t lds, hipStream_t s) {
+  if (p.p8 == 0)
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, WPE, 0>), grid, dim3(256), lds, s, p);
+  else if (p.p8 < 128)
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, WPE, 1>), grid, dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, WPE, 2>), grid, dim3(256), lds, s, p);
+}
+
 template <int HD>
 void fwd_hd(const AttnParams& p, hipStream_t s) {
-  dim3 grid((p.max_s + BLK - 1) / BLK, p.nh, p.B);
-  const size_t lds = (size_t)2 * 2 * TILE * HD * 2;
-  if (attn_occupancy().f == 3)
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 3>), grid, dim3(256), lds, s, p);
+  dim3 grid(p.nh, attn_units(p.sched ? p.n_units : 0, p.B, p.max_s));
+  const size_t lds = FwdCfg<HD>::LDS;
+  if (HD <= 64 && attn_occupancy().f == 3)  // d = 128 spills at 168 registers: 2 waves / SIMD
+    fwd_launch<HD, 3>(p, grid, lds, s);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 1>), grid, dim3(256), lds, s, p);
+    fwd_launch<HD, 1>(p, grid, lds, s);
 }
 
 template <int HD>
 void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = (int64_t)p.T * p.nh;
-  dim3 gq((p.max_s + BLK - 1) / BLK, p.nh, p.B);
-  dim3 gk((p.max_s + BLK - 1) / BLK, p.nkv, p.B);
+  const int nu = attn_units(p.sched_q ? p.n_units : 0, p.B, p.max_s);
+  dim3 gq(p.nh, nu);
+  dim3 gk(p.nkv, nu);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
   const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
   hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),

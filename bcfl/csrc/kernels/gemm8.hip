@@ -47,6 +47,7 @@
 #include "act.h"
 #include "common.h"
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace bcfl {
 namespace {
@@ -60,36 +61,8 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t g8_rsrc(const void* base, int64_t byte_off,
-                                                         int64_t nbytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base) + (uint64_t)byte_off;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  int64_t nb = nbytes < 0 ? 0 : nbytes;
-  if (nb > 0x7fffffff) nb = 0x7fffffff;
-  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)nb);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
-                                           (short)0, (int)n, 0x00020000);
-}
-
 // k-row image swizzle of a COL half-tile with 128 columns (16 chunks of 16 B per row)
 __device__ __forceinline__ int colswz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-
-#define G8_BAR()                                  \
-  do {                                            \
-    __builtin_amdgcn_sched_barrier(0);            \
-    asm volatile("s_barrier" ::: "memory");       \
-    __builtin_amdgcn_sched_barrier(0);            \
-  } while (0)
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void lgk_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
-}
 
 template <int BM, bool ACOL, bool BCOL, int EPI, int ACT>
 struct G8 {
@@ -128,7 +101,7 @@ struct G8Op {
   __device__ __forceinline__ void init(const bf16_t* base, int64_t ld, int i0, int n_valid, int k0,
                                        int k_end, int tid) {
     if constexpr (!COL) {
-      rs = g8_rsrc(base, ((int64_t)i0 * ld + k0) * 2, (int64_t)n_valid * ld * 2 - (int64_t)k0 * 2);
+      rs = buf_rsrc(base, ((int64_t)i0 * ld + k0) * 2, (int64_t)n_valid * ld * 2 - (int64_t)k0 * 2);
       kbytes = 64 * 2;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -140,7 +113,7 @@ struct G8Op {
           voff[h][j] = (int)((int64_t)(h * H + r) * ld * 2) + c * 16;
         }
     } else {
-      rs = g8_rsrc(base, (int64_t)k0 * ld * 2, (int64_t)(k_end - k0) * ld * 2);
+      rs = buf_rsrc(base, (int64_t)k0 * ld * 2, (int64_t)(k_end - k0) * ld * 2);
       kbytes = (int)(64 * ld * 2);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -157,17 +130,9 @@ struct G8Op {
   __device__ __forceinline__ void dma(char* smem, int dst, int h, int kt, int w) const {
     // the K-tile offset goes into the per-lane offset (VGPR): the range check, which zero-fills
     // k-rows past the split end, covers it
-    // (device pass only: the host pass cannot type-check the LDS-DMA builtin, and a failed
-    // host-side instantiation silently drops the kernel's launch stub)
-#if defined(__HIP_DEVICE_COMPILE__)
     const int ko = kt * kbytes;
 #pragma unroll
-    for (int j = 0; j < L; ++j) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(smem + dst + j * (T8 * 16) + w * 1024), 16,
-          voff[h][j] + ko, 0, 0, 0);
-    }
-#endif
+    for (int j = 0; j < L; ++j) dma16(rs, smem + dst + j * (T8 * 16) + w * 1024, voff[h][j] + ko);
   }
 };
 
@@ -186,19 +151,9 @@ struct G8RowRd {
   }
 };
 
-// The transposed reads are inline asm: the compiler's waitcnt pass cannot tell the
-// ds_read_tr16 builtin apart from the in-flight LDS-DMA writes and would put a vmcnt(0) (a full
-// drain of the DMA pipeline) in front of every one. hipcc does not count asm loads, so every
-// phase waits lgkmcnt(0) itself after its first barrier and then marks the fragments written
-// (g8_fence) before the MFMAs may read them.
-template <int OFF>
-__device__ __forceinline__ s16x4_t g8_tr_read(uint32_t addr) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
-  s16x4_t v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
-  return v;
-}
-
+// The transposed reads are inline asm (ds_tr_read, lds_dma.h): hipcc does not count asm loads, so
+// every phase waits lgkmcnt(0) itself after its first barrier and then marks the fragments
+// written (g8_fence) before the MFMAs may read them.
 // Transposed-read fragments of a COL operand: one 32-bit LDS base address per (16-idx block u,
 // k-half h) and lane; the buffer / half-tile / k-step offset is the instruction's immediate, so
 // the whole main loop addresses LDS with NU x 2 base registers.
@@ -219,8 +174,8 @@ struct G8ColRd {
   // HALF: byte offset of the half-tile inside the operand's LDS region; S: k-step (32 k-rows)
   template <int HALF, int S>
   __device__ __forceinline__ bf16x8_t frag(int u) const {
-    const s16x4_t lo = g8_tr_read<HALF + S * 32 * 256>(base[u][0]);
-    const s16x4_t hi = g8_tr_read<HALF + S * 32 * 256>(base[u][1]);
+    const s16x4_t lo = ds_tr_read<HALF + S * 32 * 256>(base[u][0]);
+    const s16x4_t hi = ds_tr_read<HALF + S * 32 * 256>(base[u][1]);
     const g8_s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8_t, v);
   }
@@ -361,8 +316,8 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   dmaA(1, 0, 1);
   dmaB(1, 1, 1);
   vm_wait<C::VMN>();  // K-tile 0 landed (this wave's pieces) ...
-  G8_BAR();           // ... and every wave's
-  if (wr == 1) G8_BAR();  // stagger: the second wave row runs one barrier behind
+  BCFL_BAR();           // ... and every wave's
+  if (wr == 1) BCFL_BAR();  // stagger: the second wave row runs one barrier behind
 
   // one K-tile in buffer Q: 4 phases. `full`: issue the DMAs of the K-tiles two ahead.
   using I0 = std::integral_constant<int, 0>;
@@ -376,24 +331,24 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     readA(IQ{}, I0{});
     if (Q == 0 || full) dmaA(1 - Q, 1, t + 1);
     lgk_wait<C::RA>();  // B_lo reads retired before the barrier (B_lo is re-staged in phase 2)
-    G8_BAR();
+    BCFL_BAR();
     landed(fb0, true);
     mma(0, 0, fb0);
-    G8_BAR();
+    BCFL_BAR();
     // phase 2: B_hi -> fb1; DMA B_lo (K-tile t + 2)
     readB(IQ{}, I1{}, fb1);
     if (full) dmaB(Q, 0, t + 2);
-    G8_BAR();
+    BCFL_BAR();
     landed(fb1, false);
     mma(0, 1, fb1);
-    G8_BAR();
+    BCFL_BAR();
     // phase 3: A_hi -> fa; DMA A_lo (t + 2)
     readA(IQ{}, I1{});
     if (full) dmaA(Q, 0, t + 2);
-    G8_BAR();
+    BCFL_BAR();
     landed(fb1, true);
     mma(1, 1, fb1);
-    G8_BAR();
+    BCFL_BAR();
     // phase 4: DMA B_hi (t + 2); retire everything but the last three half-tiles
     if (full) {
       dmaB(Q, 1, t + 2);
@@ -401,9 +356,9 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     } else {
       vm_wait<0>();
     }
-    G8_BAR();
+    BCFL_BAR();
     mma(1, 0, fb0);
-    G8_BAR();
+    BCFL_BAR();
   };
 
   const int iters = nt >> 1;
@@ -414,7 +369,7 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   // last pair: the even tile's phase 1 still issues the odd tile's A_hi; no further DMA
   ktile(I0{}, nt - 2, false);
   ktile(I1{}, nt - 1, false);
-  if (wr == 0) G8_BAR();  // close the stagger
+  if (wr == 0) BCFL_BAR();  // close the stagger
   lgk_wait<0>();
   __syncthreads();
 

@@ -162,6 +162,10 @@ struct AttnParams {
   uint32_t p8, ka, kb;
   uint32_t* mask = nullptr;  // dropout keep bitmask [T * nh * mask_w], WRITTEN here (if p8)
   int mask_w = 0;            // words per (token, head) row (attn_dropmask_words)
+  // work order (attn_schedule): n_units entries (b << 12) | 128-row block, longest first; null =
+  // every (b, block < ceil(max_s / 128)) in batch order
+  const int* sched = nullptr;
+  int n_units = 0;
 };
 struct AttnBwdParams {
   const void* qkv;
@@ -177,9 +181,14 @@ struct AttnBwdParams {
   uint32_t p8, ka, kb;
   const uint32_t* mask = nullptr;
   int mask_w = 0;
+  const int* sched_q = nullptr;  // query-block order (dq), as AttnParams::sched
+  const int* sched_k = nullptr;  // key-block order (dk / dv)
+  int n_units = 0;
 };
-// dropout keep bitmask, 1 bit per score: word (t * nh + h) * W + kw, bit j = keep(key 32 kw + j);
-// written by the forward, read by the backward kernels
+// dropout keep bitmask, 1 bit per score: word (t * nh + h) * W + kw holds the 32 keys
+// 32 kw + j; key j = 8 g + 4 c + e (g, e < 4, c < 2) is bit 8 e + g + 4 c (attn_mbit), the order
+// in which the forward's MFMA layout produces the decisions. Written by the forward, read by the
+// backward kernels.
 int attn_dropmask_words(int max_s);  // W
 int launch_attn_fwd(const AttnParams& p, hipStream_t s);
 

@@ -35,6 +35,8 @@ class PackedBatch:
     # table gradients then need no device sort per step
     sort_ids: Optional[torch.Tensor] = None
     sort_pos: Optional[torch.Tensor] = None
+    # optional [2, n] int32 attention work order (attn_schedule), staged with the batch
+    attn_sched: Optional[torch.Tensor] = None
 
     def order(self):
         return (self.sort_ids, self.sort_pos) if self.sort_ids is not None else None
@@ -60,7 +62,29 @@ class PackedBatch:
         mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
         return PackedBatch(mv(self.input_ids), mv(self.position_ids), mv(self.cu_seqlens),
                            mv(self.labels), self.max_seqlen, self.seq_lens, self.cu_host,
-                           mv(self.sort_ids), mv(self.sort_pos))
+                           mv(self.sort_ids), mv(self.sort_pos), mv(self.attn_sched))
+
+
+ATTN_BLOCK = 128  # rows per attention workgroup (attention.hip BLK)
+
+
+def attn_schedule(cu_host: np.ndarray, blk: int = ATTN_BLOCK) -> torch.Tensor:
+    """[2, n] int32 work order of the varlen attention kernels: one entry ``(b << 12) | block``
+    per 128-row block of every sequence (filler row included), longest sequence first (LPT: the
+    hardware dispatcher starts the long blocks at once and back-fills the short ones; in batch
+    order a long sequence late in the batch would start last and set the kernel's tail).
+    Row 0 orders query blocks (forward, dQ): within a sequence the last block first (the costliest
+    under a causal mask). Row 1 orders key blocks (dK / dV): the first block first."""
+    cu = np.asarray(cu_host, dtype=np.int64)
+    lens = cu[1:] - cu[:-1]
+    nb = (lens + blk - 1) // blk
+    b = np.repeat(np.arange(len(lens), dtype=np.int64), nb)
+    k = np.arange(int(nb.sum()), dtype=np.int64) - np.repeat(np.cumsum(nb) - nb, nb)
+    L = lens[b]
+    q_order = np.lexsort((-k, -L))   # by L desc, then block desc
+    k_order = np.lexsort((k, -L))    # by L desc, then block asc
+    enc = (b << 12) | k
+    return torch.from_numpy(np.stack([enc[q_order], enc[k_order]]).astype(np.int32))
 
 
 def _sort_order(keys: torch.Tensor) -> torch.Tensor:
@@ -73,7 +97,8 @@ def _sort_order(keys: torch.Tensor) -> torch.Tensor:
 
 def presort(b: PackedBatch) -> PackedBatch:
     return PackedBatch(b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.max_seqlen,
-                       b.seq_lens, b.cu_host, _sort_order(b.input_ids), _sort_order(b.position_ids))
+                       b.seq_lens, b.cu_host, _sort_order(b.input_ids), _sort_order(b.position_ids),
+                       b.attn_sched)
 
 
 def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
@@ -93,7 +118,7 @@ def pad_packed(b: PackedBatch, multiple: int, pad_id: int = 0) -> PackedBatch:
     pos = torch.cat([b.position_ids, torch.zeros(P, dtype=torch.int32)])
     cu = np.concatenate([b.cu_host, [T + P]])
     return PackedBatch(ids, pos, torch.from_numpy(cu.astype(np.int32)), b.labels,
-                       max(b.max_seqlen, P), b.seq_lens, cu)
+                       max(b.max_seqlen, P), b.seq_lens, cu, attn_sched=attn_schedule(cu))
 
 
 class MicroBatches(list):
@@ -143,7 +168,8 @@ def make_packed_batch(ds: TokenDataset, idx: np.ndarray) -> PackedBatch:
                        torch.from_numpy(pos.astype(np.int32)),
                        torch.from_numpy(cu.astype(np.int32)),
                        torch.from_numpy(ds.labels[idx].astype(np.int32)),
-                       int(lens.max()) if len(lens) else 0, lens, cu)
+                       int(lens.max()) if len(lens) else 0, lens, cu,
+                       attn_sched=attn_schedule(cu))
 
 
 def make_padded_batch(ds: TokenDataset, idx: np.ndarray, pad_id: int = 0) -> PaddedBatch:
@@ -215,7 +241,7 @@ class ClientLoader:
 
         def parts(b: PackedBatch):
             return [t for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.sort_ids,
-                                b.sort_pos) if t is not None]
+                                b.sort_pos, b.attn_sched) if t is not None]
 
         total = int(sum(t.numel() for b in flat for t in parts(b)))
         host = torch.empty(total, dtype=torch.int32, pin_memory=True)
@@ -235,9 +261,13 @@ class ClientLoader:
                 n = t.numel()
                 views.append(devbuf[off:off + n].view(t.shape))
                 off += n
-            so = (views[4], views[5]) if b.sort_ids is not None else (None, None)
+            i = 4
+            so = (None, None)
+            if b.sort_ids is not None:
+                so, i = (views[4], views[5]), 6
+            sched = views[i] if b.attn_sched is not None else None
             return PackedBatch(views[0], views[1], views[2], views[3], b.max_seqlen, b.seq_lens,
-                               b.cu_host, *so)
+                               b.cu_host, *so, attn_sched=sched)
 
         out = [MicroBatches(view(x) for x in b) if isinstance(b, MicroBatches) else view(b)
                for b in hb]

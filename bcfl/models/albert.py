@@ -92,7 +92,8 @@ class AlbertForSequenceClassification(SeqClassifierBase):
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
                                        c.num_attention_heads, c.num_attention_heads, c.head_dim,
-                                       c.attention_probs_dropout_prob, tr)
+                                       c.attention_probs_dropout_prob, tr,
+                                       sched=getattr(batch, "attn_sched", None))
         else:  # last application: only the pooled [CLS] rows are consumed
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
                                              c.num_attention_heads, c.num_attention_heads,

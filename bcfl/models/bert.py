@@ -82,7 +82,8 @@ class BertLayer(nn.Module):
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
                                        c.num_attention_heads, c.num_attention_heads, c.head_dim,
-                                       c.attention_probs_dropout_prob, tr)
+                                       c.attention_probs_dropout_prob, tr,
+                                       sched=getattr(batch, "attn_sched", None))
         else:
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
                                              c.num_attention_heads, c.num_attention_heads,

@@ -65,7 +65,8 @@ class DistilBertLayer(nn.Module):
         qkv = ops.linear(x, self.qkv_weight, self.qkv_bias, tap=t_attn if rows is None else None)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
-                                       c.n_heads, c.n_heads, c.head_dim, c.attention_dropout, tr)
+                                       c.n_heads, c.n_heads, c.head_dim, c.attention_dropout, tr,
+                                       sched=getattr(batch, "attn_sched", None))
         else:  # last layer: only the pooled [CLS] rows are consumed
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen,
                                              c.n_heads, c.n_heads, c.head_dim,

@@ -103,7 +103,8 @@ class LlamaLayer(nn.Module):
         qkv = ops.rope(qkv, batch.position_ids, cos, sin, nh, nkv, d)
         if rows is None:
             ctx = ops.varlen_attention(qkv, batch.cu_seqlens, batch.cu_host, batch.max_seqlen,
-                                       nh, nkv, d, 0.0, self.training, causal=True)
+                                       nh, nkv, d, 0.0, self.training, causal=True,
+                                       sched=getattr(batch, "attn_sched", None))
         else:  # last layer: only the pooled last-token rows are consumed
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen, nh,
                                              nkv, d, 0.0, self.training, causal=True)

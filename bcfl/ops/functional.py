@@ -487,12 +487,13 @@ def bias_act(y, bias, act: str = "gelu"):
 # ----------------------------------------------------------------------------------------
 class _VarlenAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cu, max_s, nh, nkv, d, scale, causal, p8, ka, kb):
+    def forward(ctx, qkv, cu, max_s, nh, nkv, d, scale, causal, p8, ka, kb, sched):
         C = native()
         out, lse, mask = C.attn_fwd(qkv, cu, int(max_s), int(nh), int(nkv), int(d), float(scale),
-                                    bool(causal), int(p8), int(ka), int(kb))
+                                    bool(causal), int(p8), int(ka), int(kb), sched)
         ctx.save_for_backward(qkv, cu, out, lse, mask)
         ctx.cfg = (max_s, nh, nkv, d, scale, causal, p8, ka, kb)
+        ctx.sched = sched
         return out
 
     @staticmethod
@@ -501,20 +502,25 @@ class _VarlenAttn(torch.autograd.Function):
         max_s, nh, nkv, d, scale, causal, p8, ka, kb = ctx.cfg
         dqkv = native().attn_bwd(dout.contiguous(), qkv, out, lse, cu, int(max_s), int(nh),
                                  int(nkv), int(d), float(scale), bool(causal), int(p8), int(ka),
-                                 int(kb), mask)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+                                 int(kb), mask, ctx.sched)
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
 def varlen_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, cu_host: Sequence[int],
                      max_seqlen: int, num_heads: int, num_kv_heads: int, head_dim: int,
                      dropout_p: float = 0.0, training: bool = False, causal: bool = False,
-                     scale: Optional[float] = None) -> torch.Tensor:
-    """qkv: [T, (nh + 2 nkv) * d] (q | k | v column blocks). Returns [T, nh * d]."""
+                     scale: Optional[float] = None,
+                     sched: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qkv: [T, (nh + 2 nkv) * d] (q | k | v column blocks). Returns [T, nh * d].
+    ``sched``: the batch's work order (:func:`bcfl.data.batching.attn_schedule`, on the device);
+    None runs the blocks in batch order."""
     scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
     p8, ka, kb = _keys(dropout_p, training)
     if use_native(qkv, "attn"):
+        if sched is not None and (not sched.is_cuda or sched.device != qkv.device):
+            sched = None
         return _VarlenAttn.apply(qkv.contiguous(), cu_seqlens, max_seqlen, num_heads,
-                                 num_kv_heads, head_dim, scale, causal, p8, ka, kb)
+                                 num_kv_heads, head_dim, scale, causal, p8, ka, kb, sched)
     return ref.varlen_attention(qkv, num_heads, num_kv_heads, head_dim, cu_host, scale, causal,
                                 p8, ka, kb)
 

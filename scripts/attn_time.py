@@ -37,13 +37,16 @@ def med(fn, n=30):
 
 
 p8, ka, kb = int(os.environ.get("P8", "26")), 12345, 678
-out, lse, mask = C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb)
-g = torch.randn_like(out)
-tf_ = med(lambda: C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb))
-tb = med(lambda: C.attn_bwd(g, qkv, out, lse, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False,
-                            p8, ka, kb, mask))
-dq = C.attn_bwd(g, qkv, out, lse, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb, mask)
-print(json.dumps({"wpe": os.environ.get("BCFL_ATTN_WPE", "1,1,1"), "T": int(b.num_tokens),
-                  "fwd_us": tf_, "bwd_us": tb, "fwd_tflops": fl / tf_ / 1e6,
-                  "bwd_tflops": 2.5 * fl / tb / 1e6,
-                  "out_sum": float(out.float().sum()), "dqkv_sum": float(dq.float().abs().sum())}))
+for sc in (None, b.attn_sched):
+    out, lse, mask = C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb, sc)
+    g = torch.randn_like(out)
+    tf_ = med(lambda: C.attn_fwd(qkv, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb, sc))
+    tb = med(lambda: C.attn_bwd(g, qkv, out, lse, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False,
+                                p8, ka, kb, mask, sc))
+    dq = C.attn_bwd(g, qkv, out, lse, b.cu_seqlens, b.max_seqlen, 12, 12, 64, 0.125, False, p8, ka, kb, mask, sc)
+    print(json.dumps({"wpe": os.environ.get("BCFL_ATTN_WPE", "3,1,1"), "sched": sc is not None,
+                      "p8": p8, "T": int(b.num_tokens),
+                      "fwd_us": tf_, "bwd_us": tb, "fwd_tflops": fl / tf_ / 1e6,
+                      "bwd_tflops": 2.5 * fl / tb / 1e6,
+                      "out_sum": float(out.float().sum()), "dqkv_sum": float(dq.float().abs().sum())}),
+          flush=True)

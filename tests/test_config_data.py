@@ -144,3 +144,24 @@ def test_compat_presets_reproduce_reference_partitions():
     cfg, tr, ps = parts("serverless_NonIID_IMDB")
     assert {int(tr.labels[p.train][0]) for p in ps} == {0, 1}
     assert all(len(np.unique(tr.labels[p.train])) == 1 for p in ps)
+
+
+def test_attn_schedule_covers_every_block_longest_first():
+    from bcfl.data.batching import attn_schedule, pad_packed
+    cu = np.array([0, 90, 603, 603, 870, 1870, 1999])
+    s = attn_schedule(cu).numpy()
+    lens = np.diff(cu)
+    want = sorted((b, k) for b in range(len(lens)) for k in range(-(-lens[b] // 128)))
+    for row in s:
+        got = [(int(e) >> 12, int(e) & 4095) for e in row]
+        assert sorted(got) == want                       # every block once, empty rows none
+        L = [lens[b] for b, _ in got]
+        assert L == sorted(L, reverse=True)              # longest sequence first
+    q = [(int(e) >> 12, int(e) & 4095) for e in s[0]][:8]
+    assert q[0] == (4, 7) and q[-1] == (4, 0)            # query blocks: last block first
+    k = [(int(e) >> 12, int(e) & 4095) for e in s[1]][:8]
+    assert k[0] == (4, 0)                                # key blocks: first block first
+    ds = load_split("tiny", "train", 2048, 128)
+    b = pad_packed(make_packed_batch(ds, np.arange(10)), 64)
+    assert b.attn_sched is not None and b.attn_sched.shape[0] == 2
+    assert int(b.attn_sched.shape[1]) == int(sum(-(-n // 128) for n in np.diff(b.cu_host)))

@@ -81,14 +81,20 @@ def test_bias_act(act):
     _grads_close([y.grad, b.grad], [yf.grad, bf.grad])
 
 
-def _attn_case(lens, nh, nkv, d, causal, p):
+def _attn_case(lens, nh, nkv, d, causal, p, sched=False, late_boost=0.0):
+    from bcfl.data.batching import attn_schedule
     torch.manual_seed(1)
     cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
     T = int(cu[-1])
-    qkv = (0.5 * torch.randn(T, (nh + 2 * nkv) * d, device=DEV)).bfloat16().requires_grad_(True)
+    x = 0.5 * torch.randn(T, (nh + 2 * nkv) * d, device=DEV)
+    if late_boost:  # keys past position 200 of every row score far above the first tile's max
+        pos = torch.from_numpy(np.concatenate([np.arange(n) for n in lens])).to(DEV)
+        x[pos > 200, nh * d:(nh + nkv) * d] *= late_boost
+    qkv = x.bfloat16().requires_grad_(True)
     cu_d = torch.from_numpy(cu).to(DEV)
+    sc = attn_schedule(cu).to(DEV) if sched else None
     rng.manual_seed(3)
-    out = ops.varlen_attention(qkv, cu_d, cu, max(lens), nh, nkv, d, p, True, causal)
+    out = ops.varlen_attention(qkv, cu_d, cu, max(lens), nh, nkv, d, p, True, causal, sched=sc)
     rng.manual_seed(3)
     p8, ka, kb = (rng.quantize_p(p), *rng.global_rng().next()) if p > 0 else (0, 0, 0)
     qf = qkv.detach().float().requires_grad_(True)
@@ -98,12 +104,36 @@ def _attn_case(lens, nh, nkv, d, causal, p):
     out.backward(go)
     r.backward(go.float())
     _grads_close([qkv.grad], [qf.grad], 3e-2)
+    return out.detach(), qkv.grad
 
 
-@pytest.mark.parametrize("lens", [[1, 5, 64, 65, 127, 128, 129], [512, 300, 200], [33]])
+@pytest.mark.parametrize("lens", [[1, 5, 64, 65, 127, 128, 129], [512, 300, 200], [33],
+                                  [1100, 700, 90]])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_bert(lens, p):
     _attn_case(lens, 12, 12, 64, False, p)
+
+
+@pytest.mark.parametrize("causal,p", [(False, 0.1), (True, 0.0)])
+def test_attention_schedule_is_bitwise(causal, p):
+    """The longest-first work order (attn_schedule) changes only WHEN a block runs: outputs and
+    gradients are bit-identical to batch order."""
+    lens = [90, 513, 7, 260, 1000, 129]
+    a = _attn_case(lens, 12, 12, 64, causal, p)
+    b = _attn_case(lens, 12, 12, 64, causal, p, sched=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_late_max_rescale(p):
+    """Scores that grow far past the first key tile's max exercise the forward's deferred
+    rescale (RESCALE_LOG2)."""
+    _attn_case([300, 450, 64], 12, 12, 64, False, p, late_boost=6.0)
+
+
+def test_attention_dropout_d32_and_causal():
+    _attn_case([1, 70, 200, 333], 4, 4, 32, False, 0.1)
+    _attn_case([1, 70, 200, 333], 4, 4, 64, True, 0.1)
 
 
 @pytest.mark.parametrize("lens", [[1, 70, 200], [256]])
