@@ -190,7 +190,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu, int6
   check_cuda(lse, "lse");
   const int T = qkv.size(0);
   auto dqkv = torch::empty_like(qkv);
-  auto delta = torch::empty({T, nh}, qkv.options().dtype(torch::kFloat));
+  // backward row constants [2, T, nh] (attention.hip attn_bwd_prep_kernel)
+  auto delta = torch::empty({2, T, nh}, qkv.options().dtype(torch::kFloat));
   bcfl::AttnBwdParams p{};
   p.qkv = qkv.data_ptr();
   p.out = out.data_ptr();

@@ -75,40 +75,6 @@ __device__ __forceinline__ float keep_and(float v, uint32_t w, int pos) {
   return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe((int)w, pos, 1));
 }
 
-// Register-staged loader of two [TILE x HD] row tiles (e.g. K and V) gathered from token rows
-// tok0 + row0 .. of two sources; rows >= L are zero-filled (so masked V rows can never be NaN).
-template <int HD>
-struct Stage2 {
-  static constexpr int CPR = HD / 8;             // 16-byte chunks per row
-  static constexpr int N = TILE * CPR / 256;     // chunks per thread per tensor
-  uint4 a[N], b[N];
-  __device__ __forceinline__ void load(const bf16_t* sa, int rsa, const bf16_t* sb, int rsb,
-                                       int tok0, int row0, int L) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int rr = idx / CPR, c = idx % CPR;
-      const int row = row0 + rr;
-      if (row < L) {
-        a[i] = *reinterpret_cast<const uint4*>(sa + (size_t)(tok0 + row) * rsa + c * 8);
-        b[i] = *reinterpret_cast<const uint4*>(sb + (size_t)(tok0 + row) * rsb + c * 8);
-      } else {
-        a[i] = make_uint4(0, 0, 0, 0);
-        b[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  }
-  __device__ __forceinline__ void store(bf16_t* da, bf16_t* db) const {  // swizzled tiles
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int o = swz_off<HD>(idx / CPR, idx % CPR);
-      *reinterpret_cast<uint4*>(da + o) = a[i];
-      *reinterpret_cast<uint4*>(db + o) = b[i];
-    }
-  }
-};
-
 // ------------------------------------------------------------------------------------------------
 // Work order. A launch is (head, unit) with unit = (sequence b, 128-row block); with a schedule
 // (attn_schedule, built on the host with the batch) units come longest-sequence first, so the
@@ -439,11 +405,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 // ------------------------------------------------------------------------------------------------
-// delta[t, h] = sum_d dO * O
+// Backward prep: per (token, head) row, the two row constants of the backward in the form the
+// kernels consume them (dropout's 1/(1-p) = sd folded in: dS = P sd (keep dP - delta / sd)):
+//   rc[0][row] = lse * log2(e) - log2(sd)   so  P sd = exp2(s * scale * log2(e) - rc0)
+//   rc[1][row] = sum_d dO * O / sd
 template <int HD>
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ dout,
-                                                        const bf16_t* __restrict__ out,
-                                                        float* __restrict__ delta, int64_t rows) {
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __restrict__ dout,
+                                                           const bf16_t* __restrict__ out,
+                                                           const float* __restrict__ lse,
+                                                           float* __restrict__ rc, int64_t rows,
+                                                           float lsd, float isd) {
   constexpr int LPR = HD / 8;  // lanes per (t, h) row
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t row = gid / LPR;
@@ -460,15 +431,22 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
   }
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-  if (row < rows && c == 0) delta[row] = a;
+  if (row < rows && c == 0) {
+    rc[row] = fmaf(lse[row], LOG2E, -lsd);
+    rc[rows + row] = a * isd;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int HD, int WPE>
+// dQ. Same K / V LDS-DMA ring as the forward. Per tile and wave (32 queries x 64 keys), for each
+// 32-key half: S^T = K Q^T and dP^T = V dO^T on MFMA (K, V row fragments by asm reads), then
+// dS = P sd (keep dP - delta / sd) from the prepped row constants and the forward's keep words
+// (prefetched one tile ahead into registers, issued before the tile's DMA so the compiler's wait
+// for them never counts the DMA down); finally dQ += dS K with K^T fragments by transposed reads.
+template <int HD, int WPE, int DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_dq_kernel(AttnBwdParams p) {
-  constexpr int STG = 2 * TILE * HD;  // K tile (row reads for S^T, transposed for dQ) | V tile
+  using C = FwdCfg<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   int b, qb;
   attn_unit(p.sched_q, blockIdx.y, p.max_s, b, qb);
@@ -477,98 +455,180 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int L = p.cu[b + 1] - tok0;
   const int q0 = qb * BLK;
   if (q0 >= L) return;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qw0 = q0 + wid * ROWS;
   const bool active = qw0 < L;
   const int hk = h / (p.nh / p.nkv);
   const int rs = (p.nh + 2 * p.nkv) * HD;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
-  const bf16_t* ksrc = qkv + p.nh * HD + hk * HD;
-  const bf16_t* vsrc = qkv + (p.nh + p.nkv) * HD + hk * HD;
   const int myq = qw0 + r;
   const int qi = min(myq, L - 1);
   const int kend = p.causal ? min(L, q0 + BLK) : L;
   const int ntiles = (kend + TILE - 1) / TILE;
 
-  Stage2<HD> stg;
-  stg.load(ksrc, rs, vsrc, rs, tok0, 0, L);
+  const __amdgpu_buffer_rsrc_t rsrc = buf_rsrc(qkv, (int64_t)tok0 * rs * 2, (int64_t)L * rs * 2);
+  int voff[2][C::PW];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int colbase = (x == 0 ? p.nh + hk : p.nh + p.nkv + hk) * HD;
+#pragma unroll
+    for (int i = 0; i < C::PW; ++i) {
+      const int c = 64 * (wid + NWAVE * i) + lane;
+      const int row = c / C::CPR;
+      const int u = (c % C::CPR) ^ swz<HD>(row);
+      voff[x][i] = row * rs * 2 + (colbase + 8 * u) * 2;
+    }
+  }
+  auto dma = [&](int st, int k0) {
+    const int ko = k0 * rs * 2;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < C::PW; ++i)
+        dma16(rsrc, smem + st * C::STG + x * C::TBYTES + (wid + NWAVE * i) * 1024, voff[x][i] + ko);
+  };
+  // keep words of this lane's query row: 2 per 64-key tile, prefetched a tile ahead
+  const uint32_t* mrow = p.mask + (size_t)((tok0 + qi) * p.nh + h) * p.mask_w;
+  u32x2_t kwn = {0u, 0u};
+  if constexpr (DROP != 0) kwn = *reinterpret_cast<const u32x2_t*>(mrow);
+  dma(0, 0);
 
   bf16x8_t qf[HD / 16], df[HD / 16];
   {
     const bf16_t* qrow = qkv + (size_t)(tok0 + qi) * rs + h * HD;
     const bf16_t* drow_ = dout + (size_t)(tok0 + qi) * p.nh * HD + h * HD;
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8_t*>(qrow + 16 * s + 8 * hh);
-      df[s] = *reinterpret_cast<const bf16x8_t*>(drow_ + 16 * s + 8 * hh);
+    for (int s2 = 0; s2 < HD / 16; ++s2) {
+      qf[s2] = *reinterpret_cast<const bf16x8_t*>(qrow + 16 * s2 + 8 * hh);
+      df[s2] = *reinterpret_cast<const bf16x8_t*>(drow_ + 16 * s2 + 8 * hh);
     }
   }
-  // dropout's 1/(1-p) is folded into P (lse shifted by log2 sd) and delta (divided by sd):
-  // dS = P sd (keep dP - delta / sd) — no per-element scale multiply.
-  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
-  const float lse2 = p.lse[(size_t)(tok0 + qi) * p.nh + h] * LOG2E - log2f(sd);
-  const float dlt = p.delta[(size_t)(tok0 + qi) * p.nh + h] / sd;
+  const size_t rrow = (size_t)(tok0 + qi) * p.nh + h;
+  const float lse2 = p.delta[rrow];
+  const float dlt = p.delta[(size_t)p.T * p.nh + rrow];
   f32x16_t dq[HD / 32];
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) dq[u] = zero16();
   const float sl2 = p.scale * LOG2E;
-  const uint32_t* mrow = p.mask + (size_t)((tok0 + qi) * p.nh + h) * p.mask_w;
 
   TileOffsets<HD> to;
   to.init(lane);
-  stg.store(lds, lds + TILE * HD);
-  __syncthreads();
+  const uint32_t lds32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  uint32_t rowb[HD / 16];
+#pragma unroll
+  for (int s2 = 0; s2 < HD / 16; ++s2) rowb[s2] = lds32 + 2 * to.row[s2];
+  uint32_t trb[HD / 32][2];  // K^T reads (K tile of stage 0)
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) trb[u][hi] = lds32 + 2 * to.tr[u][hi];
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int k0 = it * TILE;
-    const bool more = it + 1 < ntiles;
-    if (more) stg.load(ksrc, rs, vsrc, rs, tok0, k0 + TILE, L);
-    uint2 kw2 = make_uint2(0u, 0u);
-    if (p.p8) kw2 = *reinterpret_cast<const uint2*>(mrow + (k0 >> 5));
-    const bf16_t* Ks = lds + (it & 1) * STG;
-    const bf16_t* Vs = Ks + TILE * HD;
-    if (active && !(p.causal && k0 > qw0 + ROWS - 1)) {
-      f32x16_t sacc[2], pacc[2];
+  vm_wait<0>();
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        sacc[t] = zero16();
-        pacc[t] = zero16();
-#pragma unroll
-        for (int s = 0; s < HD / 16; ++s) {
-          sacc[t] = mfma32(lds_row8(Ks + 32 * t * HD + to.row[s]), qf[s], sacc[t]);
-          pacc[t] = mfma32(lds_row8(Vs + 32 * t * HD + to.row[s]), df[s], pacc[t]);
-        }
-      }
-      const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
-      bf16x8_t dsf[4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t wk = (t ? kw2.y : kw2.x) >> (4 * hh);
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          float pv = fexp2(fmaf(sacc[t][reg], sl2, -lse2));
-          if (need_mask) {
-            const int key = k0 + 32 * t + acc_row(reg, hh);
-            if (key >= L || (p.causal && key > myq)) pv = 0.f;
-          }
-          float dp = pacc[t][reg];
-          if (p.p8) dp = keep_and(dp, wk, 8 * (reg & 3) + (reg >> 2));  // key 8 (reg >> 2) + 4 hh + (reg & 3)
-          dsf[2 * t + (reg >> 3)][reg & 7] = (__bf16)(pv * (dp - dlt));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < HD / 32; ++u)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          dq[u] = mfma32(tr_operand(Ks + 16 * ks * HD, to.tr[u][0], to.tr[u][1]), dsf[ks], dq[u]);
-    }
-    if (more) {
-      bf16_t* nk = lds + ((it + 1) & 1) * STG;
-      stg.store(nk, nk + TILE * HD);
-    }
-    __syncthreads();
+  for (int s2 = 0; s2 < HD / 16; ++s2) {
+    reg_fence(qf[s2]);
+    reg_fence(df[s2]);
   }
+  BCFL_BAR();
+
+  auto tile = [&](auto stc, int it) {
+    constexpr int ST = decltype(stc)::value;
+    const int k0 = it * TILE;
+    if (it > 0) {
+      vm_wait<0>();
+      BCFL_BAR();
+    }
+    u32x2_t kw = kwn;
+    reg_fence(kw);
+    if constexpr (DROP != 0) {
+      if (it + 1 < ntiles) kwn = *reinterpret_cast<const u32x2_t*>(mrow + ((k0 + TILE) >> 5));
+    }
+    if (it + 1 < ntiles) dma(ST ^ 1, k0 + TILE);
+    if (!active || (p.causal && k0 > qw0 + ROWS - 1)) return;
+    const bool need_mask = (k0 + TILE > L) || (p.causal && k0 + TILE - 1 > qw0);
+    uint32_t dsw[4][4];  // dS as bf16 pairs, fragment ks = 2t + (reg >> 3)
+    auto half = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      bf16x8_t kf[HD / 16], vf[HD / 16];
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) kf[s2] = ds_row_read<ST * C::STG + 32 * t * HD * 2>(rowb[s2]);
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) vf[s2] = ds_row_read<ST * C::STG + C::TBYTES + 32 * t * HD * 2>(rowb[s2]);
+      lgk_wait<HD / 16>();
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) reg_fence(kf[s2]);
+      f32x16_t sacc = zero16(), pacc = zero16();
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) sacc = mfma32(kf[s2], qf[s2], sacc);
+      lgk_wait<0>();
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) reg_fence(vf[s2]);
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) pacc = mfma32(vf[s2], df[s2], pacc);
+      const uint32_t wk = (t ? kw[1] : kw[0]) >> (4 * hh);
+      if (need_mask) {
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          const int key = k0 + 32 * t + acc_row(rg, hh);
+          if (key >= L || (p.causal && key > myq)) sacc[rg] = -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {
+        float ds[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int rg = reg + e;
+          const float pv = fexp2(fmaf(sacc[rg], sl2, -lse2));
+          float dp = pacc[rg];
+          if constexpr (DROP != 0) dp = keep_and(dp, wk, 8 * (rg & 3) + (rg >> 2));  // key 8 (rg >> 2) + 4 hh + (rg & 3)
+          ds[e] = pv * (dp - dlt);
+        }
+        dsw[2 * t + (reg >> 3)][(reg & 7) >> 1] = pack2bf(ds[0], ds[1]);
+      }
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
+    // dQ += dS K: K^T fragments (k = key) by transposed reads of the stage's K tile
+    bf16x8_t kt[HD / 32][4];
+    auto kread = [&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
+      constexpr int OFF = ST * C::STG + 16 * ks * HD * 2;
+#pragma unroll
+      for (int u = 0; u < HD / 32; ++u) {
+        const s16x4_t lo = ds_tr_read<OFF>(trb[u][0]);
+        const s16x4_t hi = ds_tr_read<OFF>(trb[u][1]);
+        kt[u][ks] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    kread(std::integral_constant<int, 0>{});
+    kread(std::integral_constant<int, 1>{});
+    kread(std::integral_constant<int, 2>{});
+    kread(std::integral_constant<int, 3>{});
+    lgk_wait<0>();
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) reg_fence(kt[u][ks]);
+#pragma unroll
+    for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const uint4 w4 = make_uint4(dsw[ks][0], dsw[ks][1], dsw[ks][2], dsw[ks][3]);
+        dq[u] = mfma32(kt[u][ks], __builtin_bit_cast(bf16x8_t, w4), dq[u]);
+      }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  int it = 0;
+  for (; it + 1 < ntiles; it += 2) {
+    tile(I0{}, it);
+    tile(I1{}, it + 1);
+  }
+  if (it < ntiles) tile(I0{}, it);
   if (!active || myq >= L) return;
   bf16_t* dst = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + myq) * rs + h * HD;
 #pragma unroll
@@ -582,12 +642,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int HD, int WPE>
+// dK, dV. A wave owns 32 keys (K, V fragments and the dK^T / dV^T accumulators in registers) and
+// the workgroup sweeps every query tile of every query head of its GQA group. Per tile the LDS
+// ring stage holds, all by LDS-DMA: the Q and dO tiles (16-B pieces), the 64 prepped row
+// constants (4-B pieces: wave 0 rc0, wave 1 rc1) and each wave's 64 keep words (4-B pieces).
+template <int HD>
+struct DkdvCfg {
+  static constexpr int CPR = HD / 8;
+  static constexpr int TBYTES = TILE * HD * 2;
+  static constexpr int PW = TBYTES / 1024 / NWAVE;
+  // [stage 0 | stage 1 small arrays (rc0 256 B, rc1 256 B, keep words 1 KiB)] then
+  // [stage 0 Q | dO][stage 1 Q | dO]: every immediate LDS offset stays below 64 KiB at d = 128
+  static constexpr int SMALL = 512 + NWAVE * 256;
+  static constexpr int L0 = 0, DL0 = 256, M0 = 512;
+  static constexpr int TB = 2 * SMALL;
+  static constexpr int LDS = TB + 4 * TBYTES;
+  static constexpr int small(int st) { return st * SMALL; }
+  static constexpr int q(int st) { return TB + st * 2 * TBYTES; }
+  static constexpr int d(int st) { return TB + st * 2 * TBYTES + TBYTES; }
+};
+
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, char* lds_base, int voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_base,
+                                           4, voff, 0, 0, 0);
+#endif
+}
+
+template <int OFF>
+__device__ __forceinline__ f32x4_t ds_read_f4(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
+  f32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+
+template <int HD, int WPE, int DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_dkdv_kernel(AttnBwdParams p) {
-  // Q | dO | lse, delta (fp32 = 2 bf16 slots) | keep words [4 waves][64 queries] (uint32)
-  constexpr int STG = 2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2;
+  using C = DkdvCfg<HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   int b, kb;
   attn_unit(p.sched_k, blockIdx.y, p.max_s, b, kb);
@@ -596,15 +689,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int L = p.cu[b + 1] - tok0;
   const int kb0 = kb * BLK;
   if (kb0 >= L) return;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kw0 = kb0 + wid * ROWS;
   const bool active = kw0 < L;
   const int rs = (p.nh + 2 * p.nkv) * HD;
+  const int ds_ = p.nh * HD;  // dO row stride
   const int grp = p.nh / p.nkv;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
   const int koff = p.nh * HD + hk * HD;
-  const int voff = (p.nh + p.nkv) * HD + hk * HD;
+  const int voff_ = (p.nh + p.nkv) * HD + hk * HD;
   const int mykey = kw0 + r;
   const int ki = min(mykey, L - 1);
   const int mbit = attn_mbit(r);  // my key's bit in a keep word
@@ -612,122 +707,202 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int nqt = (L - qstart + TILE - 1) / TILE;  // q tiles per head
   const int ntiles = nqt * grp;
 
-  // dropout scale folded into the staged lse / delta exactly as in the dq kernel
-  const float sd = p.p8 ? keep_scale(p.p8) : 1.f;
-  const float lsd = log2f(sd), isd = 1.f / sd;
-  Stage2<HD> stg;
-  float ls_r = 0.f, dl_r = 0.f;  // lse / delta of row threadIdx.x (threads < TILE)
-  uint32_t mk_r = 0u;            // keep word: wave (threadIdx.x >> 6)'s key block, query tid & 63
-  auto issue = [&](int it) {
-    const int hq = hk * grp + it / nqt;
-    const int q0 = qstart + (it % nqt) * TILE;
-    stg.load(qkv + hq * HD, rs, dout + hq * HD, p.nh * HD, tok0, q0, L);
-    if (threadIdx.x < TILE) {
-      const int q = q0 + threadIdx.x;
-      ls_r = q < L ? p.lse[(size_t)(tok0 + q) * p.nh + hq] * LOG2E - lsd : 0.f;
-      dl_r = q < L ? p.delta[(size_t)(tok0 + q) * p.nh + hq] * isd : 0.f;
+  // ---- per-tile LDS-DMA sources --------------------------------------------------------------
+  const __amdgpu_buffer_rsrc_t rq = buf_rsrc(qkv, (int64_t)tok0 * rs * 2, (int64_t)L * rs * 2);
+  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dout, (int64_t)tok0 * ds_ * 2, (int64_t)L * ds_ * 2);
+  const __amdgpu_buffer_rsrc_t rc = buf_rsrc(p.delta, (int64_t)tok0 * p.nh * 4,
+                                             (int64_t)((size_t)p.T * p.nh + (size_t)L * p.nh) * 4);
+  const __amdgpu_buffer_rsrc_t rm =
+      buf_rsrc(p.mask, (int64_t)tok0 * p.nh * p.mask_w * 4, (int64_t)L * p.nh * p.mask_w * 4);
+  int qv[C::PW], dv[C::PW];
+#pragma unroll
+  for (int i = 0; i < C::PW; ++i) {
+    const int c = 64 * (wid + NWAVE * i) + lane;
+    const int row = c / C::CPR;
+    const int u = (c % C::CPR) ^ swz<HD>(row);
+    qv[i] = row * rs * 2 + 16 * u;
+    dv[i] = row * ds_ * 2 + 16 * u;
+  }
+  // rc1 rows of this sequence start T*nh floats after rc0's: only rows < L are in range for rc0
+  // (the resource's end bounds rc1), so rc0 reads past L land in rc0 of later sequences — rows
+  // >= L are masked out of every product below, whatever they hold
+  const int lv = lane * p.nh * 4;
+  const int mv = lane * p.nh * p.mask_w * 4 + ((kb0 >> 5) + wid) * 4;
+  auto dma = [&](int st, int it2) {
+    const int hq = hk * grp + it2 / nqt;
+    const int q0 = qstart + (it2 % nqt) * TILE;
+#pragma unroll
+    for (int i = 0; i < C::PW; ++i) {
+      dma16(rq, smem + C::q(st) + (wid + NWAVE * i) * 1024, qv[i] + q0 * rs * 2 + hq * HD * 2);
+      dma16(rd, smem + C::d(st) + (wid + NWAVE * i) * 1024, dv[i] + q0 * ds_ * 2 + hq * HD * 2);
     }
-    if (p.p8) {
-      const int q = q0 + (threadIdx.x & 63);
-      mk_r = q < L ? p.mask[(size_t)((tok0 + q) * p.nh + hq) * p.mask_w + (kb0 >> 5) + (threadIdx.x >> 6)]
-                   : 0u;
-    }
+    char* sm = smem + C::small(st);
+    const int rowc = (q0 * p.nh + hq) * 4;
+    if (wid == 0) dma4(rc, sm + C::L0, lv + rowc);
+    if (wid == 1) dma4(rc, sm + C::DL0, lv + rowc + p.T * p.nh * 4);
+    if constexpr (DROP != 0) dma4(rm, sm + C::M0 + wid * 256, mv + (q0 * p.nh + hq) * p.mask_w * 4);
   };
-  auto commit = [&](int buf) {
-    bf16_t* Qs = lds + buf * STG;
-    bf16_t* Ds = Qs + TILE * HD;
-    stg.store(Qs, Ds);
-    float* fs = reinterpret_cast<float*>(Ds + TILE * HD);
-    if (threadIdx.x < TILE) {
-      fs[threadIdx.x] = ls_r;
-      fs[TILE + threadIdx.x] = dl_r;
-    }
-    reinterpret_cast<uint32_t*>(fs + 2 * TILE)[threadIdx.x] = mk_r;
-  };
-  issue(0);
+  dma(0, 0);
 
   bf16x8_t kf[HD / 16], vf[HD / 16];
   {
     const bf16_t* base = qkv + (size_t)(tok0 + ki) * rs;
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8_t*>(base + koff + 16 * s + 8 * hh);
-      vf[s] = *reinterpret_cast<const bf16x8_t*>(base + voff + 16 * s + 8 * hh);
+    for (int s2 = 0; s2 < HD / 16; ++s2) {
+      kf[s2] = *reinterpret_cast<const bf16x8_t*>(base + koff + 16 * s2 + 8 * hh);
+      vf[s2] = *reinterpret_cast<const bf16x8_t*>(base + voff_ + 16 * s2 + 8 * hh);
     }
   }
-  f32x16_t dk[HD / 32], dv[HD / 32];
+  f32x16_t dk[HD / 32], dv2[HD / 32];
 #pragma unroll
-  for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv[u] = zero16(); }
+  for (int u = 0; u < HD / 32; ++u) { dk[u] = zero16(); dv2[u] = zero16(); }
   const float sl2 = p.scale * LOG2E;
 
   TileOffsets<HD> to;
   to.init(lane);
-  commit(0);
-  __syncthreads();
+  const uint32_t lds32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  uint32_t rowb[HD / 16];
+#pragma unroll
+  for (int s2 = 0; s2 < HD / 16; ++s2) rowb[s2] = lds32 + 2 * to.row[s2];
+  uint32_t trb[HD / 32][2];
+#pragma unroll
+  for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) trb[u][hi] = lds32 + 2 * to.tr[u][hi];
+  // row-constant / keep-word reads: 4 consecutive queries 8 g4 + 4 hh (+ 32 t) of the tile
+  const uint32_t cb = lds32 + 16 * hh;
+  const uint32_t mb = lds32 + wid * 256 + 16 * hh;
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int hq = hk * grp + it / nqt;
-    const int q0 = qstart + (it % nqt) * TILE;
-    const bool more = it + 1 < ntiles;
-    if (more) issue(it + 1);
-    const bf16_t* Qs = lds + (it & 1) * STG;
-    const bf16_t* Ds = Qs + TILE * HD;
-    const float* lse_s = reinterpret_cast<const float*>(Ds + TILE * HD);
-    const float* dl_s = lse_s + TILE;
-    // keep words of this wave's 32 keys (bit r = my key) for the tile's 64 queries
-    const uint32_t* mk_s = reinterpret_cast<const uint32_t*>(lse_s + 2 * TILE) + wid * TILE;
-    if (active) {
+  vm_wait<0>();
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int qt0 = q0 + 32 * t;
-        if (p.causal && qt0 + 31 < kw0) continue;  // every query of the subtile precedes my keys
-        if (qt0 >= L) continue;
-        f32x16_t sacc = zero16(), pacc = zero16();
-#pragma unroll
-        for (int s = 0; s < HD / 16; ++s) {
-          sacc = mfma32(lds_row8(Qs + 32 * t * HD + to.row[s]), kf[s], sacc);
-          pacc = mfma32(lds_row8(Ds + 32 * t * HD + to.row[s]), vf[s], pacc);
-        }
-        const bool need_mask = (qt0 + 32 > L) || (p.causal && qt0 < kw0 + ROWS);
-        bf16x8_t pf[2], dsf[2];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int ql = 32 * t + 8 * g4 + 4 * hh;  // 4 consecutive queries
-          const float4 ls4 = *reinterpret_cast<const float4*>(lse_s + ql);
-          const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + ql);
-          const float lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
-          uint4 m4 = make_uint4(0u, 0u, 0u, 0u);
-          if (p.p8) m4 = *reinterpret_cast<const uint4*>(mk_s + ql);
-          const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int reg = 4 * g4 + e;
-            const int q = q0 + ql + e;
-            float pv = fexp2(fmaf(sacc[reg], sl2, -lsv[e]));  // = P / (1 - p)
-            if (need_mask && (q >= L || (p.causal && mykey > q))) pv = 0.f;
-            float pd = pv, dp = pacc[reg];
-            if (p.p8) {
-              const int km = __builtin_amdgcn_sbfe((int)mw[e], mbit, 1);
-              pd = __int_as_float(__float_as_int(pv) & km);
-              dp = __int_as_float(__float_as_int(dp) & km);
-            }
-            pf[reg >> 3][reg & 7] = (__bf16)pd;
-            dsf[reg >> 3][reg & 7] = (__bf16)(pv * (dp - dlv[e]));
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < HD / 32; ++u)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int kb = (32 * t + 16 * s2) * HD;
-            dv[u] = mfma32(tr_operand(Ds + kb, to.tr[u][0], to.tr[u][1]), pf[s2], dv[u]);
-            dk[u] = mfma32(tr_operand(Qs + kb, to.tr[u][0], to.tr[u][1]), dsf[s2], dk[u]);
-          }
-      }
-    }
-    if (more) commit((it + 1) & 1);
-    __syncthreads();
+  for (int s2 = 0; s2 < HD / 16; ++s2) {
+    reg_fence(kf[s2]);
+    reg_fence(vf[s2]);
   }
+  BCFL_BAR();
+
+  auto tile = [&](auto stc, int it2) {
+    constexpr int ST = decltype(stc)::value;
+    const int q0 = qstart + (it2 % nqt) * TILE;
+    if (it2 > 0) {
+      vm_wait<0>();
+      BCFL_BAR();
+    }
+    if (it2 + 1 < ntiles) dma(ST ^ 1, it2 + 1);
+    if (!active) return;
+    auto half = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const int qt0 = q0 + 32 * t;
+      if (p.causal && qt0 + 31 < kw0) return;  // every query of the subtile precedes my keys
+      if (qt0 >= L) return;
+      bf16x8_t qr[HD / 16], dr[HD / 16];
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) qr[s2] = ds_row_read<C::q(ST) + 32 * t * HD * 2>(rowb[s2]);
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) dr[s2] = ds_row_read<C::d(ST) + 32 * t * HD * 2>(rowb[s2]);
+      f32x4_t lc[4], dc[4];
+      u32x4_t mw[4];
+      static_for<4>([&](auto gc) {
+        constexpr int g4 = decltype(gc)::value;
+        lc[g4] = ds_read_f4<C::small(ST) + C::L0 + (32 * t + 8 * g4) * 4>(cb);
+        dc[g4] = ds_read_f4<C::small(ST) + C::DL0 + (32 * t + 8 * g4) * 4>(cb);
+        if constexpr (DROP != 0)
+          mw[g4] = __builtin_bit_cast(u32x4_t, ds_read_f4<C::small(ST) + C::M0 + (32 * t + 8 * g4) * 4>(mb));
+      });
+      lgk_wait<0>();
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) {
+        reg_fence(qr[s2]);
+        reg_fence(dr[s2]);
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        reg_fence(lc[g4]);
+        reg_fence(dc[g4]);
+        if constexpr (DROP != 0) reg_fence(mw[g4]);
+      }
+      f32x16_t sacc = zero16(), pacc = zero16();
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 16; ++s2) {
+        sacc = mfma32(qr[s2], kf[s2], sacc);
+        pacc = mfma32(dr[s2], vf[s2], pacc);
+      }
+      if ((qt0 + 32 > L) || (p.causal && qt0 < kw0 + ROWS)) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int q = qt0 + acc_row(reg, hh);
+          if (q >= L || (p.causal && mykey > q)) sacc[reg] = -INFINITY;
+        }
+      }
+      uint32_t pw[2][4], dw[2][4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        float pd[4], dsv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int reg = 4 * g4 + e;
+          const float pv = fexp2(fmaf(sacc[reg], sl2, -lc[g4][e]));  // = P sd
+          float pdv = pv, dp = pacc[reg];
+          if constexpr (DROP != 0) {
+            const int km = __builtin_amdgcn_sbfe((int)mw[g4][e], mbit, 1);
+            pdv = __int_as_float(__float_as_int(pv) & km);
+            dp = __int_as_float(__float_as_int(dp) & km);
+          }
+          pd[e] = pdv;
+          dsv[e] = pv * (dp - dc[g4][e]);
+        }
+        pw[g4 >> 1][2 * (g4 & 1)] = pack2bf(pd[0], pd[1]);
+        pw[g4 >> 1][2 * (g4 & 1) + 1] = pack2bf(pd[2], pd[3]);
+        dw[g4 >> 1][2 * (g4 & 1)] = pack2bf(dsv[0], dsv[1]);
+        dw[g4 >> 1][2 * (g4 & 1) + 1] = pack2bf(dsv[2], dsv[3]);
+      }
+      // dV^T += dO^T P, dK^T += Q^T dS: dO^T / Q^T fragments by transposed reads
+      bf16x8_t dt[HD / 32][2], qt[HD / 32][2];
+      auto trd = [&](auto s2c) {
+        constexpr int s2 = decltype(s2c)::value;
+        constexpr int KB = (32 * t + 16 * s2) * HD * 2;
+#pragma unroll
+        for (int u = 0; u < HD / 32; ++u) {
+          const s16x4_t a0 = ds_tr_read<C::d(ST) + KB>(trb[u][0]);
+          const s16x4_t a1 = ds_tr_read<C::d(ST) + KB>(trb[u][1]);
+          dt[u][s2] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+          const s16x4_t b0 = ds_tr_read<C::q(ST) + KB>(trb[u][0]);
+          const s16x4_t b1 = ds_tr_read<C::q(ST) + KB>(trb[u][1]);
+          qt[u][s2] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      };
+      trd(std::integral_constant<int, 0>{});
+      trd(std::integral_constant<int, 1>{});
+      lgk_wait<0>();
+#pragma unroll
+      for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          reg_fence(dt[u][s2]);
+          reg_fence(qt[u][s2]);
+        }
+#pragma unroll
+      for (int u = 0; u < HD / 32; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const uint4 a = make_uint4(pw[s2][0], pw[s2][1], pw[s2][2], pw[s2][3]);
+          const uint4 c2 = make_uint4(dw[s2][0], dw[s2][1], dw[s2][2], dw[s2][3]);
+          dv2[u] = mfma32(dt[u][s2], __builtin_bit_cast(bf16x8_t, a), dv2[u]);
+          dk[u] = mfma32(qt[u][s2], __builtin_bit_cast(bf16x8_t, c2), dk[u]);
+        }
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  int it = 0;
+  for (; it + 1 < ntiles; it += 2) {
+    tile(I0{}, it);
+    tile(I1{}, it + 1);
+  }
+  if (it < ntiles) tile(I0{}, it);
   if (!active || mykey >= L) return;
   bf16_t* drow = reinterpret_cast<bf16_t*>(p.dqkv) + (size_t)(tok0 + mykey) * rs;
 #pragma unroll
@@ -736,16 +911,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int g4 = 0; g4 < 4; ++g4) {
       const float kv[4] = {dk[u][4 * g4] * p.scale, dk[u][4 * g4 + 1] * p.scale,
                            dk[u][4 * g4 + 2] * p.scale, dk[u][4 * g4 + 3] * p.scale};
-      const float vv[4] = {dv[u][4 * g4], dv[u][4 * g4 + 1], dv[u][4 * g4 + 2], dv[u][4 * g4 + 3]};
+      const float vv[4] = {dv2[u][4 * g4], dv2[u][4 * g4 + 1], dv2[u][4 * g4 + 2], dv2[u][4 * g4 + 3]};
       Vec4<bf16_t>::store(drow + koff + 32 * u + 8 * g4 + 4 * hh, kv);
-      Vec4<bf16_t>::store(drow + voff + 32 * u + 8 * g4 + 4 * hh, vv);
+      Vec4<bf16_t>::store(drow + voff_ + 32 * u + 8 * g4 + 4 * hh, vv);
     }
 }
 
 }  // namespace
 
 // "F,Q,K" minimum waves per SIMD of the fwd / dq / dkdv kernels (each 1 or 3; scripts/attn_time.py)
-struct AttnOcc { int f = 3, q = 1, k = 1; };  // measured: fwd 73.8 -> 70.6 us; dq, dkdv slower at 3
+struct AttnOcc { int f = 3, q = 1, k = 1; };  // minimum waves / SIMD: 3 = at most 168 registers (d <= 64)
 const AttnOcc& attn_occupancy() {
   static const AttnOcc o = [] {
     AttnOcc a;
@@ -779,27 +954,31 @@ void fwd_hd(const AttnParams& p, hipStream_t s) {
     fwd_launch<HD, 1>(p, grid, lds, s);
 }
 
+template <int HD, int DROP>
+void bwd_launch(const AttnBwdParams& p, hipStream_t s) {
+  const int nu = attn_units(p.sched_q ? p.n_units : 0, p.B, p.max_s);
+  const AttnOcc& o = attn_occupancy();
+  if (HD <= 64 && o.q == 3)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 3, DROP>), dim3(p.nh, nu), dim3(256), FwdCfg<HD>::LDS, s, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1, DROP>), dim3(p.nh, nu), dim3(256), FwdCfg<HD>::LDS, s, p);
+  if (HD <= 64 && o.k == 3)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 3, DROP>), dim3(p.nkv, nu), dim3(256), DkdvCfg<HD>::LDS, s, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1, DROP>), dim3(p.nkv, nu), dim3(256), DkdvCfg<HD>::LDS, s, p);
+}
+
 template <int HD>
 void bwd_hd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = (int64_t)p.T * p.nh;
-  const int nu = attn_units(p.sched_q ? p.n_units : 0, p.B, p.max_s);
-  dim3 gq(p.nh, nu);
-  dim3 gk(p.nkv, nu);
-  const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
-  const bf16_t* out = reinterpret_cast<const bf16_t*>(p.out);
-  hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
-                     dim3(256), 0, s, dout, out, p.delta, rows);
-  const AttnOcc& o = attn_occupancy();
-  const size_t lq = (size_t)2 * 2 * TILE * HD * 2;
-  if (o.q == 3)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 3>), gq, dim3(256), lq, s, p);
+  const float sd = p.p8 ? 256.0f / (256.0f - (float)p.p8) : 1.f;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel<HD>, dim3((unsigned)((rows * (HD / 8) + 255) / 256)),
+                     dim3(256), 0, s, reinterpret_cast<const bf16_t*>(p.dout),
+                     reinterpret_cast<const bf16_t*>(p.out), p.lse, p.delta, rows, log2f(sd), 1.f / sd);
+  if (p.p8)
+    bwd_launch<HD, 1>(p, s);
   else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), gq, dim3(256), lq, s, p);
-  const size_t lk = (size_t)2 * (2 * TILE * HD + 2 * TILE * 2 + NWAVE * TILE * 2) * 2;
-  if (o.k == 3)
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 3>), gk, dim3(256), lk, s, p);
-  else
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(256), lk, s, p);
+    bwd_launch<HD, 0>(p, s);
 }
 
 int attn_dropmask_words(int max_s) {

@@ -16,6 +16,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 MFMA acc
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 

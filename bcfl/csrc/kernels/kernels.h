@@ -172,7 +172,7 @@ struct AttnBwdParams {
   const void* out;
   const void* dout;    // [T, nh * d]
   const float* lse;    // [T, nh]
-  float* delta;        // [T, nh] scratch: rowsum(dO * O)
+  float* delta;        // [2, T, nh] scratch: the prepped row constants (lse, rowsum(dO * O))
   void* dqkv;          // [T, (nh + 2 nkv) * d]
   const int* cu;
   int B, T, nh, nkv, d, max_s;

@@ -14,6 +14,8 @@
 //   * BCFL_BAR(): a raw s_barrier fenced against compiler reordering (a __syncthreads() would also
 //     drain the DMA queue).
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace bcfl {
@@ -70,6 +72,26 @@ __device__ __forceinline__ bf16x8_t ds_row_read(uint32_t addr) {
 template <typename T>
 __device__ __forceinline__ void reg_fence(T& v) {
   asm volatile("" : "+v"(v));
+}
+
+// f(std::integral_constant<int, I>{}) for I = 0 .. N-1: loop indices that must be compile-time
+// (immediate LDS offsets)
+template <int I, int N>
+struct StaticFor {
+  template <class F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    StaticFor<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct StaticFor<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&) {}
+};
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  StaticFor<0, N>::run(f);
 }
 
 #define BCFL_BAR()                                \
