@@ -722,7 +722,7 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   Tensor db, dbp;
   if (with_bias) {
     db = torch::empty({N}, g.options());
-    dbp = torch::empty({g8 ? std::max(S, bcfl::wgrad_g8_bias_parts(M)) : S, N},
+    dbp = torch::empty({g8 ? bcfl::wgrad_g8_bias_parts(S) : S, N},
                        g.options().dtype(torch::kFloat));
     p.dbias_part = dbp.data_ptr<float>();
     p.dbias = db.data_ptr();

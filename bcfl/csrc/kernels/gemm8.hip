@@ -250,6 +250,14 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
         for (int j = 0; j < TJ; ++j) acc[a][bb][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   bf16x8_t fa[TI][2], fb0[TJ][2], fb1[TJ][2];
+  // bias gradient (A COL): wave column wc sums A half (wc & 1), k-half (wc >> 1) of each K-tile
+  const bool rs_on = ACOL && p.rowsum != nullptr && n0 == 0;  // workgroup-uniform
+  f32x4_t rsacc[ACOL ? TI : 1];
+#pragma unroll
+  for (int i = 0; i < (ACOL ? TI : 1); ++i) rsacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
   auto readA = [&](auto qc, auto ac) {
     constexpr int q = decltype(qc)::value, a = decltype(ac)::value;
@@ -289,6 +297,17 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[a][bh][i][j] = mfma16(fa[i][s], fb[j][s], acc[a][bh][i][j]);
+    if constexpr (ACOL) {
+      if (rs_on && bh == 0 && a == (wc & 1)) {  // sum_k A(m, k) = (A . ones)(m, *)
+        if (wc >> 1) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) rsacc[i] = mfma16(fa[i][1], ones, rsacc[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) rsacc[i] = mfma16(fa[i][0], ones, rsacc[i]);
+        }
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   // after a phase's first barrier: its LDS reads have landed (asm transposed reads are not
@@ -372,6 +391,19 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   if (wr == 0) BCFL_BAR();  // close the stagger
   lgk_wait<0>();
   __syncthreads();
+
+  if constexpr (ACOL) {
+    if (rs_on && (lane & 15) == 0) {  // column 0 of each 16 x 16 row-sum tile
+      float* rsp = p.rowsum + (int64_t)(2 * split + (wc >> 1)) * p.M;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + (wc & 1) * HA + wr * QM + 16 * i + (lane >> 4) * 4 + r;
+          if (m < p.M) rsp[m] = rsacc[i][r];
+        }
+    }
+  }
 
   // ---- epilogue: per-wave LDS slab, 16-byte row segments ------------------------------------
   constexpr int LDF = QN + 4;  // slab row stride (floats)
@@ -466,48 +498,14 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
   return 0;
 }
 
-// bias gradient partials of the weight-gradient path: bpart[b, n] = sum of G[m, n] over the
-// CS rows of row block b (fp32). A workgroup covers 256 columns x CS rows: 32 column groups of 8
-// (16-byte loads) x 8 row lanes, CS / 8 independent loads in flight per thread, the 8 row lanes
-// reduced through LDS. The deterministic reduce kernel sums the row blocks.
-constexpr int CS_ROWS = 128;
-__global__ __launch_bounds__(256) void g8_colsum_kernel(const bf16_t* __restrict__ G, int64_t ldg,
-                                                        int M, int N, float* __restrict__ bpart) {
-  __shared__ float red[8][256 + 4];
-  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
-  const int n8 = blockIdx.x * 256 + cg * 8;
-  const int m0 = blockIdx.y * CS_ROWS;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (n8 < N) {
-#pragma unroll 4
-    for (int r = rl; r < CS_ROWS; r += 8) {
-      const int m = m0 + r;
-      if (m < M) {
-        float v[8];
-        Vec8<bf16_t>::load(G + (int64_t)m * ldg + n8, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += v[e];
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) red[rl][cg * 8 + e] = acc[e];
-  __syncthreads();
-  const int col = threadIdx.x;  // 256 columns of this block, one per thread
-  float t = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t += red[k][col];
-  const int n = blockIdx.x * 256 + col;
-  if (n < N) bpart[(int64_t)blockIdx.y * N + n] = t;
-}
-
 }  // namespace
 
 // Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
 // B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers
 // about half the chip (the other half stays free for the dgrad / attention kernels running
 // concurrently on the compute stream or other client lanes); fp32 slice partials are summed by
-// the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials.
+// the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials the
+// n-tile-0 workgroups produce in the main loop (G^T . ones on MFMA: no second pass over G).
 int wgrad_g8_splits(int M, int N, int K, int* Mc) {
   if (N % BN8 || K % BN8 || N <= 0 || M <= 0) return 0;
   static const int slots = [] {
@@ -537,21 +535,17 @@ int launch_wgrad_g8(const WgradParams& p, hipStream_t s) {
   g.kc = p.Mc;
   g.epi = p.S > 1 ? EPI_PARTIAL : EPI_STORE;
   g.part = p.part;
+  g.rowsum = p.dbias ? p.dbias_part : nullptr;  // bias gradient fused: 2 partial rows per split
   int rc = launch_g8(g, s);
   if (rc) return rc;
-  const int SB = wgrad_g8_bias_parts(p.M);
-  if (p.dbias) {
-    const dim3 cg((p.N + 255) / 256, SB);
-    hipLaunchKernelGGL(g8_colsum_kernel, cg, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(p.G),
-                       p.ldg, p.M, p.N, p.dbias_part);
-  }
+  const int SB = 2 * p.S;
   if (p.S > 1 || p.dbias)
     return launch_wgrad_reduce(p.S > 1 ? p.part : nullptr, p.S, p.N, p.K, p.out, p.ldo,
                                p.dbias ? p.dbias_part : nullptr, p.dbias, s, SB);
   return 0;
 }
 
-int wgrad_g8_bias_parts(int M) { return (M + CS_ROWS - 1) / CS_ROWS; }
+int wgrad_g8_bias_parts(int S) { return 2 * S; }
 
 // Block-row choice: a launch takes ceil(tiles / 256 CUs) waves of tiles, a 128-row tile takes
 // ~0.57 of a 256-row tile's time (measured 1.15x less efficient per FLOP). Pick the smaller

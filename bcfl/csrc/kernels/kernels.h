@@ -100,7 +100,7 @@ int launch_wgrad(const WgradParams& p, hipStream_t s);
 // out[n, k] = bf16(sum_s part[s, n, k]); with bpart: dbias[n] = bf16(sum_s bpart[s, n])
 int launch_wgrad_reduce(const float* part, int S, int N, int K, void* out, int64_t ldo,
                         const float* bpart, void* dbias, hipStream_t s, int SB = 0);
-int wgrad_g8_bias_parts(int M);  // rows of the bias-partial buffer the g8 weight gradient needs
+int wgrad_g8_bias_parts(int S);  // rows of the bias-partial buffer the g8 weight gradient needs
 // weight gradient on the 8-phase kernel (gemm8.hip, both operands transposed-read): split count
 // for an M x N x K problem (0 = shape not supported) and the launch (p.S / p.Mc from it)
 int wgrad_g8_splits(int M, int N, int K, int* Mc);
@@ -142,6 +142,10 @@ struct G8Params {
   const void* bias = nullptr;    // [N] bf16
   void* aux = nullptr;           // [M, N] bf16 (EPI_BIAS_ACT writes, EPI_DACT reads)
   int64_t ldaux = 0;
+  // A COL (weight gradient, A = G^T) only: row sums of A over each split's K range, i.e. the bias
+  // gradient sum_rows G, by MFMA against a ones operand in the n-tile-0 workgroups:
+  // rowsum[(2 split + h) * M + m], h = the two k-halves of every K-tile (summed by the reduce)
+  float* rowsum = nullptr;
   float* part = nullptr;         // EPI_PARTIAL: fp32 [splits, M, ldc]
   int splits = 1;
   int kc = 0;                    // reduction elements per split (multiple of 128 for ROW operands)

@@ -27,7 +27,13 @@ def category(n: str) -> str:
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"):
         return "GEMM (hipBLASLt)"
     if "bcfl" in n:
-        return "bcfl HIP kernels (LN / act / AdamW / gossip / SHA)"
+        if re.search(r"g8_|wgrad|linear_|gemm|colsum", n):
+            return "GEMM (bcfl MFMA: g8 / K9 wgrad + reductions)"
+        if "ln" in n.lower() or "layernorm" in n.lower():
+            return "LayerNorm family (bcfl)"
+        if "adamw" in n:
+            return "AdamW (bcfl multi-tensor)"
+        return "other bcfl HIP kernels (act / xent / gossip / SHA / mix)"
     if "at::native" in n:
         return "torch eager kernels"
     return "runtime copies / fills"
