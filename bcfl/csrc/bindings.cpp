@@ -691,7 +691,10 @@ bool gemm_native_ok(int64_t M, int64_t N, int64_t K, bool nn, bool accum) {
 
 // ------------------------------------------------------------------------------------------------
 namespace {
-bool g_wgrad_g8 = false;
+// the 8-phase kernel in every regime: >= the K9 kernel with lanes (0.598 vs 0.608 s/round, 2 reps
+// each) and on the overlapped single-client step, and the only one whose lane / overlap runs are
+// bitwise (profiles/lanes_bitwise_diag_r3.txt); set_wgrad_kernel(false) keeps K9 selectable
+bool g_wgrad_g8 = true;
 }
 void set_wgrad_kernel(bool g8) { g_wgrad_g8 = g8; }
 
@@ -706,8 +709,7 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   int Mc = 0;
   // the 8-phase kernel (gemm8.hip) for 256-multiple shapes, the K9 kernel (gemm.hip) otherwise
   // kernel choice: BCFL_WGRAD_G8=0/1 (read per call: A/B switchable at run time) overrides the
-  // regime default set by set_wgrad_kernel() (ops.set_wgrad_overlap: g8 when the weight gradients
-  // run on the side stream beside the dgrad chain, K9 when concurrent lanes fill the GPU)
+  // default set by set_wgrad_kernel() (g8)
   const char* env_g8 = std::getenv("BCFL_WGRAD_G8");
   const bool use_g8 = env_g8 && *env_g8 ? env_g8[0] != '0' : g_wgrad_g8;
   int S = use_g8 ? bcfl::wgrad_g8_splits(M, N, K, &Mc) : 0;

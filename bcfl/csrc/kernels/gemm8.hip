@@ -502,16 +502,17 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
 
 // Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
 // B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers
-// about half the chip (the other half stays free for the dgrad / attention kernels running
-// concurrently on the compute stream or other client lanes); fp32 slice partials are summed by
+// about a quarter of the chip (64 tile slots: the rest stays free for the dgrad / attention
+// kernels running concurrently on the compute stream or other client lanes, and fewer slices
+// mean less fp32 partial traffic); fp32 slice partials are summed by
 // the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials the
 // n-tile-0 workgroups produce in the main loop (G^T . ones on MFMA: no second pass over G).
 int wgrad_g8_splits(int M, int N, int K, int* Mc) {
   if (N % BN8 || K % BN8 || N <= 0 || M <= 0) return 0;
   static const int slots = [] {
     const char* e = std::getenv("BCFL_G8_WGRAD_SLOTS");
-    const int v = e ? std::atoi(e) : 128;
-    return v > 0 ? v : 128;
+    const int v = e ? std::atoi(e) : 64;  // 1-client round: 64 slots 0.0927 s, 128 0.0942, 256 0.0968
+    return v > 0 ? v : 64;
   }();
   const int tiles = (N / BN8) * (K / BN8);  // 256 x 256 output tiles of dW[N, K]
   int S = (slots + tiles - 1) / tiles;

@@ -64,16 +64,9 @@ _WG = {"enabled": False, "side": {}}
 
 
 def set_wgrad_overlap(enabled: bool) -> None:
-    """Side-stream weight gradients on / off. Also picks the weight-gradient kernel for the
-    regime: overlapped (one client at a time, e.g. the 8-GPU layout) -> the 8-phase kernel at
-    half the chip's width (gemm8.hip, 1-client round -4 %); concurrent client lanes -> the K9
-    split-M kernel (profiles/g8_wgrad_vs_k9.json, scripts/gpu_ab_wgrad.sh)."""
+    """Side-stream weight gradients on / off (the weight-gradient kernel is the 8-phase one in
+    both regimes; ``native().set_wgrad_kernel(False)`` / BCFL_WGRAD_G8=0 select the K9 kernel)."""
     _WG["enabled"] = bool(enabled)
-    try:
-        if torch.cuda.is_available():
-            native().set_wgrad_kernel(bool(enabled))
-    except RuntimeError:
-        pass
 
 
 def wgrad_overlap_enabled() -> bool:
