@@ -168,6 +168,14 @@ def main():
               "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
               "mixed": sum(float(h.get("mixed") or 0.0) for h in timed)}
         multi = {"per_rank": D.all_gather_object(ex)}
+    # what one client update weighs on the wire (trainable parameters only: LoRA runs exchange
+    # adapters) and what each rank actually sent per timed round (max over ranks)
+    wire = 2 if (cfg.wire_dtype if cfg.mode == "serverless" else cfg.server_wire_dtype) == "bf16" else 4
+    sent = [float(h.get("bytes_sent") or 0.0) for h in timed]
+    exchange = {"trainable_params": int(fed.flat.num_params),
+                "update_payload_bytes": int(fed.flat.numel) * wire,
+                "wire_dtype": "bf16" if wire == 2 else "fp32",
+                "bytes_sent_per_round_max_over_ranks": D.max_over_ranks(sum(sent) / max(len(sent), 1))}
     ck = fed.ckpt
     # measured peer-copy times of the mailbox posts (multi-rank runs: one model update to one
     # peer over xGMI), read before finish() closes the transport
@@ -231,6 +239,7 @@ def main():
                                                  and ck.skipped == 0,
                        "gossip_transport": fed.transport},
             "checkpoints": {"saved": ck.saved if ck else 0, "skipped": ck.skipped if ck else 0},
+            "exchange": exchange,
             "p2p_post_measured": p2p,
             "info_passing": info,
             "ledger": {"height": len(fed.ledger) if fed.ledger else 0,
