@@ -699,7 +699,7 @@ bool g_wgrad_g8 = true;
 void set_wgrad_kernel(bool g8) { g_wgrad_g8 = g8; }
 
 // dW[N, K] = g[M, N]^T x[M, K] (bf16 in/out, fp32 accumulate); rows may be strided views
-std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
+std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias, int64_t slots = 0) {
   TORCH_CHECK(g.is_cuda() && x.is_cuda(), "wgrad: GPU tensors required");
   TORCH_CHECK(g.dim() == 2 && x.dim() == 2 && g.size(0) == x.size(0), "wgrad: g [M,N], x [M,K]");
   TORCH_CHECK(g.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16");
@@ -712,7 +712,7 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   // default set by set_wgrad_kernel() (g8)
   const char* env_g8 = std::getenv("BCFL_WGRAD_G8");
   const bool use_g8 = env_g8 && *env_g8 ? env_g8[0] != '0' : g_wgrad_g8;
-  int S = use_g8 ? bcfl::wgrad_g8_splits(M, N, K, &Mc) : 0;
+  int S = use_g8 ? bcfl::wgrad_g8_splits(M, N, K, &Mc, (int)slots) : 0;
   const bool g8 = S >= 1;
   if (!g8) S = bcfl::wgrad_splits(M, N, K, &Mc);
   TORCH_CHECK(S >= 1, "wgrad: N and K must be multiples of 128");
@@ -734,7 +734,7 @@ std::vector<Tensor> wgrad_impl(Tensor g, Tensor x, bool with_bias) {
   return {out};
 }
 
-Tensor wgrad(Tensor g, Tensor x) { return wgrad_impl(g, x, false)[0]; }
+Tensor wgrad(Tensor g, Tensor x, int64_t slots) { return wgrad_impl(g, x, false, slots)[0]; }
 
 // (dW, db) with db = colsum(g) fused into the weight-gradient kernel
 std::vector<Tensor> wgrad_bias(Tensor g, Tensor x) { return wgrad_impl(g, x, true); }
@@ -805,7 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_bwd", &bdaln_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
-  m.def("wgrad", &wgrad);
+  m.def("wgrad", &wgrad, py::arg("g"), py::arg("x"), py::arg("slots") = 0);
   m.def("linear_fwd", &linear_fwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_stats", &xent_stats);

@@ -507,13 +507,14 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
 // mean less fp32 partial traffic); fp32 slice partials are summed by
 // the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials the
 // n-tile-0 workgroups produce in the main loop (G^T . ones on MFMA: no second pass over G).
-int wgrad_g8_splits(int M, int N, int K, int* Mc) {
+int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override) {
   if (N % BN8 || K % BN8 || N <= 0 || M <= 0) return 0;
-  static const int slots = [] {
+  static const int slots_env = [] {
     const char* e = std::getenv("BCFL_G8_WGRAD_SLOTS");
     const int v = e ? std::atoi(e) : 64;  // 1-client round: 64 slots 0.0927 s, 128 0.0942, 256 0.0968
     return v > 0 ? v : 64;
   }();
+  const int slots = slots_override > 0 ? slots_override : slots_env;
   const int tiles = (N / BN8) * (K / BN8);  // 256 x 256 output tiles of dW[N, K]
   int S = (slots + tiles - 1) / tiles;
   const int maxS = M / 1024 > 0 ? M / 1024 : 1;  // keep >= 16 K-tiles per slice

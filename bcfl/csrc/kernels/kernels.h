@@ -103,7 +103,7 @@ int launch_wgrad_reduce(const float* part, int S, int N, int K, void* out, int64
 int wgrad_g8_bias_parts(int S);  // rows of the bias-partial buffer the g8 weight gradient needs
 // weight gradient on the 8-phase kernel (gemm8.hip, both operands transposed-read): split count
 // for an M x N x K problem (0 = shape not supported) and the launch (p.S / p.Mc from it)
-int wgrad_g8_splits(int M, int N, int K, int* Mc);
+int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override = 0);  // slots: 0 = default
 int launch_wgrad_g8(const WgradParams& p, hipStream_t s);
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------

@@ -93,6 +93,29 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_fwd_kernel(
 // The next row's dout / z / stats are loaded into registers before the current row's reductions
 // (two rows in flight per wave: one memory round-trip hidden behind each row's math), and the
 // dropout hash is evaluated once per 4 consecutive elements (bcfl/ops/rng.py keep layout).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ln_rsrc(const void* base, int64_t nbytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(nbytes > 0x7fffffff ? 0x7fffffff : nbytes));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, (int)n, 0x00020000);
+}
+template <typename TA>
+__device__ __forceinline__ void ln_load4(__amdgpu_buffer_rsrc_t r, int off, float v[4]);
+template <>
+__device__ __forceinline__ void ln_load4<bf16_t>(__amdgpu_buffer_rsrc_t r, int off, float v[4]) {
+  const u32x2_t x = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  v[0] = __uint_as_float(x[0] << 16); v[1] = __uint_as_float(x[0] & 0xffff0000u);
+  v[2] = __uint_as_float(x[1] << 16); v[3] = __uint_as_float(x[1] & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void ln_load4<float>(__amdgpu_buffer_rsrc_t r, int off, float v[4]) {
+  const u32x4_t x = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  v[0] = __uint_as_float(x[0]); v[1] = __uint_as_float(x[1]);
+  v[2] = __uint_as_float(x[2]); v[3] = __uint_as_float(x[3]);
+}
+
 template <typename TA, typename TP, int NCH>
 __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
     const TA* __restrict__ dout, const TA* __restrict__ z, const float* __restrict__ mean_in,
@@ -118,32 +141,40 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
   }
   const int stride = gridDim.x * LN_WAVES;
   int row = blockIdx.x * LN_WAVES + wid;
-  float nd[NCH][4], nz[NCH][4], nmean = 0.f, nrstd = 0.f;
-  auto fetch = [&](int r) {
-    if (r < T) {
-      const size_t bs = (size_t)r * H;
-      nmean = mean_in[r];
-      nrstd = rstd_in[r];
+  // two rows in flight ahead of the one being reduced (buffers A / B alternate): ~3 rows x 3 KB
+  // of loads per wave outstanding — the wave-per-row loop is latency-bound at ~2 waves / SIMD
+  struct RowBuf {
+    float d[NCH][4], z[NCH][4], mean, rstd;
+  };
+  RowBuf ba, bb;
+  // unconditional buffer loads (rows >= T and columns >= H read zeros from the range check): no
+  // control flow around the loads, so the compiler's vmcnt waits count exactly and never drain
+  // the rows still in flight
+  const __amdgpu_buffer_rsrc_t rd = ln_rsrc(dout, (int64_t)T * H * (int64_t)sizeof(TA));
+  const __amdgpu_buffer_rsrc_t rz = ln_rsrc(z, (int64_t)T * H * (int64_t)sizeof(TA));
+  const __amdgpu_buffer_rsrc_t rmn = ln_rsrc(mean_in, (int64_t)T * 4);
+  const __amdgpu_buffer_rsrc_t rrs = ln_rsrc(rstd_in, (int64_t)T * 4);
+  auto fetch = [&](RowBuf& nb, int r) {
+    const int rr = r < T ? r : T;  // past the end: offset T * H -> zeros (and no int overflow)
+    nb.mean = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmn, rr * 4, 0, 0));
+    nb.rstd = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, rr * 4, 0, 0));
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        const int col = (lane + i * WAVE) * 4;
-        if (col < H) {
-          Vec4<TA>::load(dout + bs + col, nd[i]);
-          Vec4<TA>::load(z + bs + col, nz[i]);
-        }
-      }
+    for (int i = 0; i < NCH; ++i) {
+      const int col = (lane + i * WAVE) * 4;
+      const int off = (rr * H + (col < H ? col : H * T)) * (int)sizeof(TA);
+      ln_load4<TA>(rd, off, nb.d[i]);
+      ln_load4<TA>(rz, off, nb.z[i]);
     }
   };
-  fetch(row);
-  for (; row < T; row += stride) {
-    const size_t base = (size_t)row * H;
-    const float mean = nmean, rstd = nrstd;
+  auto process = [&](RowBuf& cb, int r) {
+    const size_t base = (size_t)r * H;
+    const float mean = cb.mean, rstd = cb.rstd;
     float d[NCH][4], xh[NCH][4], g[NCH][4];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { d[i][k] = nd[i][k]; xh[i][k] = nz[i][k]; }
-    fetch(row + stride);  // in flight during this row's math
+      for (int k = 0; k < 4; ++k) { d[i][k] = cb.d[i][k]; xh[i][k] = cb.z[i][k]; }
+    fetch(cb, r + 2 * stride);  // refill this buffer two rows ahead, in flight during the math
     uint32_t hs[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
@@ -182,6 +213,12 @@ __global__ __launch_bounds__(LN_THREADS) void bdaln_bwd_kernel(
         if (dy_out) Vec4<TA>::store(dy_out + base + col, dy);
       }
     }
+  };
+  fetch(ba, row);
+  fetch(bb, row + stride);
+  for (; row < T; row += 2 * stride) {
+    process(ba, row);
+    if (row + stride < T) process(bb, row + stride);
   }
   // combine the block's waves
 #pragma unroll
