@@ -189,25 +189,46 @@ __device__ __forceinline__ void g8_fence(bf16x8_t (&f)[N][2]) {
     for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(f[i][s]));
 }
 
-template <int BM, bool ACOL, bool BCOL, int EPI, int ACT>
+template <int BM, bool ACOL, bool BCOL, int EPI, int ACT, bool PERSIST>
 __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   using C = G8<BM, ACOL, BCOL, EPI, ACT>;
   constexpr int TI = C::TI, TJ = C::TJ, QM = C::QM, QN = C::QN, HA = C::HA, HB = C::HB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- tile / split assignment (XCD-aware: each XCD walks a contiguous range of tiles) -------
+  // The hardware puts workgroup b on XCD b % 8; XCD x owns logical tiles [xbase, xbase + xcnt).
+  // One-shot grids (grid = tiles x splits) take logical tile xbase + b / 8. PERSIST grids
+  // (a multiple of 8 workgroups, one per CU) walk their XCD's range with stride grid / 8, and
+  // issue the next tile's prologue DMA before the current tile's epilogue (separate epilogue
+  // slab): the DMA latency and the workgroup relaunch leave the critical path.
   const int tilesN = p.N / BN8;
   const int tilesM = (p.M + BM - 1) / BM;
   const int ntile = tilesM * tilesN;
   const int nwg = ntile * p.splits;
   const int b = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
-  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int tile = L / p.splits, split = L - tile * p.splits;
-  const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN8;
-  const int kbeg = split * p.kc;
-  const int kend = min(p.K, kbeg + p.kc);
-  const int nt = ((kend - kbeg + 127) / 128) * 2;  // K-tiles, even
+  const int xbase = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcnt = q8 + (xcd < r8 ? 1 : 0);
+  const int jstep = PERSIST ? (int)(gridDim.x >> 3) : xcnt;
+  int jt = b >> 3;
+  if (jt >= xcnt) return;  // workgroup-uniform (PERSIST grids larger than an XCD's share)
+
+  struct TileC {
+    int m0, n0, split, kbeg, kend, nt;
+  };
+  auto coords = [&](int jj) {
+    const int L = xbase + jj;
+    const int tile = L / p.splits;
+    TileC c;
+    c.split = L - tile * p.splits;
+    c.m0 = (tile / tilesN) * BM;
+    c.n0 = (tile % tilesN) * BN8;
+    c.kbeg = c.split * p.kc;
+    c.kend = min(p.K, c.kbeg + p.kc);
+    c.nt = ((c.kend - c.kbeg + 127) / 128) * 2;  // K-tiles, even
+    return c;
+  };
+  TileC cur = coords(jt);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -219,10 +240,13 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   G8Op<BCOL, HB> opB;
   const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
   const bf16_t* B = reinterpret_cast<const bf16_t*>(p.B);
-  if constexpr (!ACOL) opA.init(A, p.lda, m0, min(BM, p.M - m0), kbeg, kend, tid);
-  else opA.init(A, p.lda, m0, 0, kbeg, kend, tid);
-  if constexpr (!BCOL) opB.init(B, p.ldb, n0, min(BN8, p.N - n0), kbeg, kend, tid);
-  else opB.init(B, p.ldb, n0, 0, kbeg, kend, tid);
+  auto init_ops = [&](const TileC& c) {
+    if constexpr (!ACOL) opA.init(A, p.lda, c.m0, min(BM, p.M - c.m0), c.kbeg, c.kend, tid);
+    else opA.init(A, p.lda, c.m0, 0, c.kbeg, c.kend, tid);
+    if constexpr (!BCOL) opB.init(B, p.ldb, c.n0, min(BN8, p.N - c.n0), c.kbeg, c.kend, tid);
+    else opB.init(B, p.ldb, c.n0, 0, c.kbeg, c.kend, tid);
+  };
+  init_ops(cur);
 
   // LDS byte offsets: buffer q, A half a / B half b
   // LDS: A region [buffer 0 half 0 | b0 h1 | b1 h0 | b1 h1], then the B region the same way
@@ -251,7 +275,7 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
 
   bf16x8_t fa[TI][2], fb0[TJ][2], fb1[TJ][2];
   // bias gradient (A COL): wave column wc sums A half (wc & 1), k-half (wc >> 1) of each K-tile
-  const bool rs_on = ACOL && p.rowsum != nullptr && n0 == 0;  // workgroup-uniform
+  bool rs_on = ACOL && p.rowsum != nullptr && cur.n0 == 0;  // workgroup-uniform
   f32x4_t rsacc[ACOL ? TI : 1];
 #pragma unroll
   for (int i = 0; i < (ACOL ? TI : 1); ++i) rsacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -327,13 +351,16 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   auto dmaB = [&](int q, int bh, int kt) { opB.dma(smem, b_half(q, bh), bh, kt, w); };
 
   // ---- prologue: K-tile 0 (all four half-tiles) + K-tile 1 (B_lo, A_lo, B_hi) ---------------
-  dmaB(0, 0, 0);
-  dmaA(0, 0, 0);
-  dmaB(0, 1, 0);
-  dmaA(0, 1, 0);
-  dmaB(1, 0, 1);
-  dmaA(1, 0, 1);
-  dmaB(1, 1, 1);
+  auto prologue = [&]() {
+    dmaB(0, 0, 0);
+    dmaA(0, 0, 0);
+    dmaB(0, 1, 0);
+    dmaA(0, 1, 0);
+    dmaB(1, 0, 1);
+    dmaA(1, 0, 1);
+    dmaB(1, 1, 1);
+  };
+  prologue();
   vm_wait<C::VMN>();  // K-tile 0 landed (this wave's pieces) ...
   BCFL_BAR();           // ... and every wave's
   if (wr == 1) BCFL_BAR();  // stagger: the second wave row runs one barrier behind
@@ -380,100 +407,171 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     BCFL_BAR();
   };
 
-  const int iters = nt >> 1;
-  for (int it = 0; it < iters - 1; ++it) {
-    ktile(I0{}, 2 * it, true);
-    ktile(I1{}, 2 * it + 1, true);
-  }
-  // last pair: the even tile's phase 1 still issues the odd tile's A_hi; no further DMA
-  ktile(I0{}, nt - 2, false);
-  ktile(I1{}, nt - 1, false);
-  if (wr == 0) BCFL_BAR();  // close the stagger
-  lgk_wait<0>();
-  __syncthreads();
-
-  if constexpr (ACOL) {
-    if (rs_on && (lane & 15) == 0) {  // column 0 of each 16 x 16 row-sum tile
-      float* rsp = p.rowsum + (int64_t)(2 * split + (wc >> 1)) * p.M;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + (wc & 1) * HA + wr * QM + 16 * i + (lane >> 4) * 4 + r;
-          if (m < p.M) rsp[m] = rsacc[i][r];
-        }
-    }
-  }
-
-  // ---- epilogue: per-wave LDS slab, 16-byte row segments ------------------------------------
+  // ---- epilogue of tile c: per-wave LDS slab, 16-byte row segments --------------------------
+  // (PERSIST: the slab sits past the operand buffers, which the next tile's prologue fills)
   constexpr int LDF = QN + 4;  // slab row stride (floats)
-  float* slab = reinterpret_cast<float*>(smem) + w * (QM * LDF);
+  float* slab = reinterpret_cast<float*>(smem + (PERSIST ? C::LDS : 0)) + w * (QM * LDF);
   constexpr int LPR = QN / 8;           // lanes per slab row
   constexpr int RPP = 64 / LPR;         // rows per pass
   const int rr0 = lane / LPR, cc = (lane % LPR) * 8;
   bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C);
   bf16_t* aux = reinterpret_cast<bf16_t*>(p.aux);
   const bf16_t* bias = reinterpret_cast<const bf16_t*>(p.bias);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
+  // bias of the tile's columns, loaded before the next tile's prologue DMA is issued (a load
+  // issued after it would make the compiler drain that DMA before the first bias use)
+  float bvs[2][8];
+  auto load_bias = [&](const TileC& c) {
 #pragma unroll
     for (int bh = 0; bh < 2; ++bh) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            slab[(16 * i + (lane >> 4) * 4 + r) * LDF + 16 * j + (lane & 15)] = acc[a][bh][i][j][r];
-      const int n = n0 + bh * HB + wc * QN + cc;
-      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 8; ++e) bvs[bh][e] = 0.f;
       if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ACT) {
-        if (bias) Vec8<bf16_t>::load(bias + n, bv);
+        if (bias) Vec8<bf16_t>::load(bias + c.n0 + bh * HB + wc * QN + cc, bvs[bh]);
       }
+    }
+  };
+  auto epilogue = [&](const TileC& c) {
+    if constexpr (ACOL) {
+      if (rs_on && (lane & 15) == 0) {  // column 0 of each 16 x 16 row-sum tile
+        float* rsp = p.rowsum + (int64_t)(2 * c.split + (wc >> 1)) * p.M;
 #pragma unroll
-      for (int ps = 0; ps < QM / RPP; ++ps) {
-        const int rr = rr0 + ps * RPP;
-        const int m = m0 + a * HA + wr * QM + rr;
-        float v[8];
-        Vec8<float>::load(slab + rr * LDF + cc, v);
-        if (m < p.M) {
-          if constexpr (EPI == EPI_PARTIAL) {
-            float* dst = p.part + ((int64_t)split * p.M + m) * p.ldc + n;
-            Vec8<float>::store(dst, v);
-          } else {
-            if constexpr (EPI == EPI_BIAS) {
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] += bv[e];
-            } else if constexpr (EPI == EPI_BIAS_ACT) {
+          for (int r = 0; r < 4; ++r) {
+            const int m = c.m0 + (wc & 1) * HA + wr * QM + 16 * i + (lane >> 4) * 4 + r;
+            if (m < p.M) rsp[m] = rsacc[i][r];
+          }
+      }
+    }
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] + bv[e]));  // pre, as stored
-              Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + n, v);
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = act_ft<ACT>(v[e]);
-            } else if constexpr (EPI == EPI_DACT) {
-              float av[8];
-              Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, av);
+      for (int bh = 0; bh < 2; ++bh) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] *= act_dt<ACT>(av[e]);
-            } else if constexpr (EPI == EPI_ACCUM) {
-              float ov[8];
-              Vec8<bf16_t>::load(Cp + (int64_t)m * p.ldc + n, ov);
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] += ov[e];
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              slab[(16 * i + (lane >> 4) * 4 + r) * LDF + 16 * j + (lane & 15)] = acc[a][bh][i][j][r];
+        const int n = c.n0 + bh * HB + wc * QN + cc;
+        const float* bv = bvs[bh];
+#pragma unroll
+        for (int ps = 0; ps < QM / RPP; ++ps) {
+          const int rr = rr0 + ps * RPP;
+          const int m = c.m0 + a * HA + wr * QM + rr;
+          float v[8];
+          if constexpr (PERSIST) {
+            // asm reads: the compiler would drain the next tile's DMA (vmcnt(0)) in front of a
+            // C++ LDS read while it is in flight
+            const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(slab + rr * LDF + cc);
+            f32x4_t lo, hi;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(ad) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(hi) : "v"(ad) : "memory");
+            lgk_wait<0>();
+            reg_fence(lo);
+            reg_fence(hi);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = lo[e];
+              v[4 + e] = hi[e];
             }
-            Vec8<bf16_t>::store(Cp + (int64_t)m * p.ldc + n, v);
+          } else {
+            Vec8<float>::load(slab + rr * LDF + cc, v);
+          }
+          if (m < p.M) {
+            if constexpr (EPI == EPI_PARTIAL) {
+              float* dst = p.part + ((int64_t)c.split * p.M + m) * p.ldc + n;
+              Vec8<float>::store(dst, v);
+            } else {
+              if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += bv[e];
+              } else if constexpr (EPI == EPI_BIAS_ACT) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] + bv[e]));  // pre, as stored
+                Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + n, v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = act_ft<ACT>(v[e]);
+              } else if constexpr (EPI == EPI_DACT) {
+                float av[8];
+                Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, av);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] *= act_dt<ACT>(av[e]);
+              } else if constexpr (EPI == EPI_ACCUM) {
+                float ov[8];
+                Vec8<bf16_t>::load(Cp + (int64_t)m * p.ldc + n, ov);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += ov[e];
+              }
+              Vec8<bf16_t>::store(Cp + (int64_t)m * p.ldc + n, v);
+            }
           }
         }
       }
+  };
+
+  while (true) {
+    const int iters = cur.nt >> 1;
+    for (int it = 0; it < iters - 1; ++it) {
+      ktile(I0{}, 2 * it, true);
+      ktile(I1{}, 2 * it + 1, true);
     }
+    // last pair: the even tile's phase 1 still issues the odd tile's A_hi; no further DMA
+    ktile(I0{}, cur.nt - 2, false);
+    ktile(I1{}, cur.nt - 1, false);
+    if (wr == 0) BCFL_BAR();  // close the stagger
+    lgk_wait<0>();
+    if constexpr (!PERSIST) {
+      __syncthreads();
+      load_bias(cur);
+      epilogue(cur);
+      break;
+    } else {
+      const int jn = jt + jstep;
+      const bool more = jn < xcnt;  // workgroup-uniform
+      load_bias(cur);
+      BCFL_BAR();  // every wave is done reading the operand buffers
+      TileC nxt = cur;
+      if (more) {  // next tile's prologue in flight under this tile's epilogue
+        nxt = coords(jn);
+        init_ops(nxt);
+        prologue();
+      }
+      epilogue(cur);
+      if (!more) break;
+      jt = jn;
+      cur = nxt;
+      rs_on = ACOL && p.rowsum != nullptr && cur.n0 == 0;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[a][bb][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr (ACOL) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) rsacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+      vm_wait<0>();  // the next tile's K-tiles 0 / 1 (and this epilogue's stores) have landed
+      BCFL_BAR();
+      if (wr == 1) BCFL_BAR();  // re-open the stagger
+    }
+  }
 }
 
-template <int BM, bool ACOL, bool BCOL>
-int g8_dispatch(const G8Params& p, hipStream_t s) {
-  const int ntile = ((p.M + BM - 1) / BM) * (p.N / BN8);
-  const dim3 grid(ntile * p.splits), block(T8);
-  constexpr size_t lds = G8<BM, ACOL, BCOL, 0, 0>::LDS;
-#define G8_L(E, A) hipLaunchKernelGGL((g8_kernel<BM, ACOL, BCOL, E, A>), grid, block, lds, s, p)
+// persistent grid (one workgroup per CU, BM = 128 only: 96 KiB of operand buffers + the 36 KiB
+// epilogue slab) when the launch has more tiles than CUs; BCFL_G8_PERSIST=0/1 overrides
+bool g8_persist_default = false;
+
+template <int BM, bool ACOL, bool BCOL, bool PERSIST>
+int g8_dispatch_t(const G8Params& p, hipStream_t s, int nwg) {
+  constexpr int SLAB = T8 / 64 * G8<BM, ACOL, BCOL, 0, 0>::QM * (G8<BM, ACOL, BCOL, 0, 0>::QN + 4) * 4;
+  constexpr size_t lds = G8<BM, ACOL, BCOL, 0, 0>::LDS + (PERSIST ? SLAB : 0);
+  const dim3 grid(PERSIST ? 256 : nwg), block(T8);
+#define G8_L(E, A) hipLaunchKernelGGL((g8_kernel<BM, ACOL, BCOL, E, A, PERSIST>), grid, block, lds, s, p)
   switch (p.epi) {
     case EPI_STORE: G8_L(EPI_STORE, 0); break;
     case EPI_BIAS: G8_L(EPI_BIAS, 0); break;
@@ -498,7 +596,20 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
   return 0;
 }
 
+template <int BM, bool ACOL, bool BCOL>
+int g8_dispatch(const G8Params& p, hipStream_t s) {
+  const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN8) * p.splits;
+  bool persist = g8_persist_default;
+  if (const char* e = std::getenv("BCFL_G8_PERSIST")) persist = e[0] == '1';
+  if constexpr (BM == 128) {
+    if (persist && nwg > 256) return g8_dispatch_t<BM, ACOL, BCOL, true>(p, s, nwg);
+  }
+  return g8_dispatch_t<BM, ACOL, BCOL, false>(p, s, nwg);
+}
+
 }  // namespace
+
+void set_g8_persistent(bool on) { g8_persist_default = on; }
 
 // Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
 // B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers

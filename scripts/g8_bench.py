@@ -32,10 +32,11 @@ def mk(M, N, K, a_col, b_col, dev, seed=0):
 def check(dev):
     C = native()
     res = []
-    cases = [  # M, N, K, a_col, b_col, bm
+    cases = [  # M, N, K, a_col, b_col, bm  (the last three: > 256 tiles, persistent grids)
         (512, 256, 128, 0, 0, 256), (1000, 768, 768, 0, 0, 256), (2304, 2304, 768, 0, 0, 256),
         (777, 512, 3072, 0, 0, 256), (512, 768, 256, 0, 1, 256), (1000, 768, 2304, 0, 1, 256),
         (640, 3072, 768, 0, 1, 256), (384, 768, 768, 0, 0, 128), (300, 512, 384, 0, 1, 128),
+        (7680, 2304, 768, 0, 0, 128), (7777, 3072, 768, 0, 1, 128), (9000, 1024, 512, 0, 0, 128),
     ]
     for M, N, K, ac, bc, bm in cases:
         A, B = mk(M, N, K, ac, bc, dev, seed=M + N + K)

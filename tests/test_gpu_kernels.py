@@ -377,15 +377,11 @@ def test_linear_autograd_uses_wgrad_kernel():
 
 
 
-@pytest.mark.parametrize("model", [
-    pytest.param("bert-base-2l", marks=pytest.mark.xfail(
-        reason="with side-stream weight gradients the layer-0 / embedding gradients differ from "
-               "the inline path by 1e-6..1e-4 (reduction order, timing-dependent; "
-               "scripts/overlap_diag.py); deterministic=True turns the overlap off", strict=False)),
-    "albert-base-v2"])
+@pytest.mark.parametrize("model", ["bert-base-2l", "albert-base-v2"])
 def test_overlapped_wgrad_matches_inline(model):
-    """Side-stream weight gradients (K9 on a paired stream, joined before the optimizer) give
-    bit-identical parameter gradients to the inline path; ALBERT's shared layer opts out."""
+    """Side-stream weight gradients (the 8-phase kernel on a paired stream, joined before the
+    optimizer) give bit-identical parameter gradients to the inline path; ALBERT's shared layer
+    opts out."""
     from bcfl.data.batching import make_packed_batch
     from bcfl.data.registry import load_split
     from bcfl.models import build_model, special_tokens
