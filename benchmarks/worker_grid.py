@@ -44,6 +44,13 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
             torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     fed.drain()
+    fed.timer.resolve(block=True)
+    steady_h = fed.history[3:] if len(fed.history) > 4 else fed.history
+    phases = {}
+    for h in steady_h:
+        for k, v in h.items():
+            if (k.startswith("t_") or k.startswith("dev_t_")) and isinstance(v, (int, float)):
+                phases[k] = phases.get(k, 0.0) + float(v) / len(steady_h)
     fa = fed.federation_accuracy()
     fed.finish()
     steady = times[3:] if len(times) > 4 else times
@@ -54,7 +61,8 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
            "final_accuracy": fa.get("accuracy"), "global_eval_rows": fa.get("rows"),
            "final_majority_rate": fed.history[-1].get("global_majority_rate"),
            "accuracy_curve": list(fed.global_accuracies), "lanes": len(fed.lanes) or 1,
-           "hbm_peak_gb": fed.history[-1].get("hbm_peak_gb")}
+           "hbm_peak_gb": fed.history[-1].get("hbm_peak_gb"),
+           "steady_phase_means_s": phases}
     del fed
     gc.collect()
     if torch.cuda.is_available():
