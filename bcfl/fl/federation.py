@@ -766,16 +766,17 @@ class Federation:
         forward passes over the global draw run concurrently with round r+1's training (with one
         client per GPU — the 8-GPU layout — a training step leaves most CUs idle between
         kernels). The evaluated model, rows and kernels are exactly those of the inline path;
-        only the host read is deferred (``_resolve_eval``). Collective mode keeps the inline
-        path (its statistics are all-reduced)."""
+        only the host read is deferred (``_resolve_eval``). In collective mode (server FedAvg
+        over RCCL, lock-step gossip) the statistics are all-reduced at that deferred read, which
+        every rank reaches at the same point of its program."""
         cfg = self.cfg
         self._eval_pending = None
         self.eval_model = self.eval_flat = self.eval_trainer = self.eval_stream = None
         on = cfg.overlap_global_eval
         if on is None:
             big = self.flat.numel > 1_000_000_000
-            on = self.is_cuda and self.collective_free and not big and not cfg.deterministic
-        if not (on and cfg.eval_global and self.is_cuda and self.collective_free):
+            on = self.is_cuda and not big and not cfg.deterministic and not cfg.compat_chain
+        if not (on and cfg.eval_global and self.is_cuda):
             return
         self.eval_model = build_model(cfg.model, self.num_labels, device=self.device, dtype=mdtype,
                                       dropout=cfg.dropout, vocab_size=vocab, seed=cfg.seed,
@@ -831,6 +832,8 @@ class Federation:
         r, acc, _sets, ev, t_beg = p
         ev.synchronize()
         self.timer.add_hidden("eval_global", t_beg.elapsed_time(ev) / 1000.0)
+        if not self.collective_free:
+            D.all_reduce_(acc)
         a = acc.cpu().tolist()
         ge = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
         self._note_global_counts(r, a)
@@ -961,7 +964,12 @@ class Federation:
                     loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
                 client_metrics = self._gather_metrics(loc)
         agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
-        ge = self._eval_global(r) if cfg.eval_global else None
+        ge = None
+        if cfg.eval_global:
+            if self.eval_stream is not None:
+                self._launch_eval_global(r)   # the global model, scored beside round r + 1
+            else:
+                ge = self._eval_global(r)
         train_loss = self._reduce_train_loss(losses)
         extra = {"kind": "global", "root": self._merkle() if self.ledger else "",
                  "rejected": sorted(v.rejected)}

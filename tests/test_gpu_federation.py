@@ -107,17 +107,18 @@ def test_gpu_concurrent_llama_shaped_gemms_complete():
             assert torch.equal(outs[i][j], ref[i][j])
 
 
-def test_gpu_overlapped_global_eval_matches_inline(tmp_path):
+@pytest.mark.parametrize("mode", ["serverless", "server"])
+def test_gpu_overlapped_global_eval_matches_inline(tmp_path, mode):
     """Global evaluation on the side stream (snapshot + eval replica, result filed one round
     later) scores the same model on the same rows as the inline path, and the training it
-    overlaps is unaffected (same client states)."""
+    overlaps is unaffected (same client states / global model)."""
     from bcfl.config import FLConfig
     from bcfl.fl import Federation
     from bcfl.parallel import dist as D
     outs = []
     for ov in (False, True):
         D.set_runtime_for_tests(None)
-        cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=4,
+        cfg = FLConfig(mode=mode, model="bert-base-2l", dataset="imdb", num_clients=4,
                        num_rounds=3, train_samples=64, test_samples=32, global_test_samples=96,
                        out_dir=str(tmp_path / str(ov)), reference_prints=False, save_every=0,
                        client_lanes=1, overlap_wgrad=False, dropout=0.1,
@@ -125,9 +126,11 @@ def test_gpu_overlapped_global_eval_matches_inline(tmp_path):
         fed = Federation(cfg, verbose=False)
         assert (fed.eval_stream is not None) == ov
         h = fed.run()
+        state = (torch.stack([fed.client_master[c] for c in range(4)]) if mode == "serverless"
+                 else fed.global_master.unsqueeze(0))
         outs.append(([r["global_acc"] for r in h], [r["global_loss"] for r in h],
                      [r["global_eval_rows"] for r in h], list(fed.global_accuracies),
-                     torch.stack([fed.client_master[c] for c in range(4)]).cpu()))
+                     state.cpu()))
         D.set_runtime_for_tests(None)
     (a_acc, a_loss, a_rows, a_g, a_m), (b_acc, b_loss, b_rows, b_g, b_m) = outs
     assert None not in b_acc and b_rows == a_rows == [96] * 3
