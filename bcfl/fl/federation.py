@@ -1196,6 +1196,12 @@ class Federation:
         cfg = self.cfg
         if self.ckpt is None or (r + 1) % cfg.save_every:
             return
+        pend = self._eval_pending
+        if pend is not None and pend[0] == r and not self.collective_free and self.rt.distributed:
+            # multi-rank collective mode: the saved accuracy is the job's (all-reduced), so
+            # resolve here, where every rank is (before the per-rank busy-skip below); one rank
+            # holds the whole job's statistics and leaves this to the writer thread
+            self._resolve_eval()
         if self.ckpt.busy():
             if cfg.save_resume_state:
                 # resumable runs never skip: every rank's files of a save belong to ONE round
