@@ -490,6 +490,29 @@ class Federation:
                 ops.weighted_accumulate_(self.acc, a, 1.0)
         return out
 
+    def _server_eval_local(self, r: int, G: torch.Tensor) -> Dict[int, torch.Tensor]:
+        """Flower's evaluate_round: every hosted client scores the new global model G on its own
+        test split. With client lanes the clients' evaluations run concurrently, each lane's
+        replica holding G (lane 0's flat buffer already does); otherwise one after another.
+        Device tensors [correct, count, loss_sum, batch_mean_sum] per client, no host sync."""
+        if len(self.lanes) <= 1:
+            return {c: self.trainer.evaluate_device(self.test_batches(c, r))
+                    for c in self.local_clients}
+        main = torch.cuda.current_stream(self.device) if self.is_cuda else None
+        res: Dict[int, torch.Tensor] = {}
+        for ln in self.lanes:
+            if ln.stream is not None:
+                ln.stream.wait_stream(main)  # G is final on the main stream
+            with self._on(ln):
+                if ln.flat is not self.flat:
+                    ln.flat.load_master(G)   # the next round's lane worker reloads G anyway
+                for c in ln.clients:
+                    res[c] = ln.trainer.evaluate_device(self.test_batches(c, r))
+        for ln in self.lanes:
+            if ln.stream is not None:
+                main.wait_stream(ln.stream)
+        return res
+
     # ================================ helpers ==================================================
     def log(self, *a):
         if self.verbose:
@@ -954,9 +977,7 @@ class Federation:
         client_metrics = []
         if cfg.eval_local:
             with self.timer.phase("eval_local"):
-                dev_res = {}
-                for c in self.local_clients:
-                    dev_res[c] = self.trainer.evaluate_device(self.test_batches(c, r))
+                dev_res = self._server_eval_local(r, G)
                 loc = []
                 for c, t in dev_res.items():
                     a = t.cpu().tolist()

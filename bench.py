@@ -71,6 +71,8 @@ def parse():
                     help="skip the post-run information-passing measurement (N > 1)")
     ap.add_argument("--global-test-samples", type=int, default=0,
                     help="override the global evaluation draw (experiments only; 0 = preset)")
+    ap.add_argument("--batch-size", type=int, default=0,
+                    help="override the preset's local batch size (0 = preset)")
     ap.add_argument("--micro-batches", type=int, default=0,
                     help="ranks training one client at a time: 2 = concurrent micro-batches, 1 = off, 0 = auto")
     return ap.parse_args()
@@ -116,6 +118,7 @@ def main():
                      save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
                      device=a.device, client_lanes=a.lanes, micro_batches=a.micro_batches,
                      overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad),
+                     **({"batch_size": a.batch_size} if a.batch_size > 0 else {}),
                      **({"global_test_samples": a.global_test_samples}
                         if a.global_test_samples > 0 else {}),
                      **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}))
@@ -227,7 +230,8 @@ def main():
             "samples_per_s": a.clients * cfg.train_samples * a.steps / dt,
             "dtype": "bf16" if fed.dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (IMDB-shaped lengths, label-sorted Non-IID shards, packed varlen); random-init weights",
-            "config": {"model": a.model, "global_batch": 32 * a.clients, "seq_len": 512,
+            "config": {"model": a.model, "global_batch": cfg.batch_size * a.clients,
+                       "seq_len": cfg.max_seq_len,
                        "parallelism": f"fl{a.clients}-clients-on-{rt.world}gpu",
                        "clients": a.clients, "mode": a.mode,
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,

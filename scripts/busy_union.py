@@ -1,10 +1,11 @@
 """GPU busy fraction from a rocprofv3 kernel trace: union of kernel [start, end) intervals over the
-trace's span, plus the largest idle gaps (is the device ever waiting on the host?)."""
+trace's span, plus the largest idle gaps (is the device ever waiting on the host?). Several trace
+files (one per rank process sharing the GPU) are merged into one timeline."""
 import csv
 import json
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+rows = [r for f in sys.argv[1:] for r in csv.DictReader(open(f))]
 iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows)
 # skip the first 40 % of the trace (start-up, compilation, warm-up rounds)
 t0 = iv[0][0] + int(0.4 * (iv[-1][1] - iv[0][0]))
