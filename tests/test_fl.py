@@ -378,3 +378,5 @@ def test_server_lanes_match_sequential(tmp_out, lanes):
     assert float((a.global_master - b.global_master).abs().max()) < 1e-6
     assert [h["train_loss"] for h in ha] == pytest.approx([h["train_loss"] for h in hb], rel=1e-5)
     assert [h["global_acc"] for h in ha] == [h["global_acc"] for h in hb]
+    # Flower's evaluate_round on the lanes: every client scores the same global model
+    assert [h["distributed_acc"] for h in ha] == [h["distributed_acc"] for h in hb]
