@@ -678,6 +678,64 @@ void linear_fwd_acc(Tensor x, Tensor w, Tensor into) {
   check_rc(bcfl::launch_linear_nt(p, stream()), "linear_fwd_acc");
 }
 
+// Frozen base projection + LoRA low-rank product in ONE 8-phase GEMM, the low-rank factors
+// appended to the reduction as a tail segment (no [M, N] delta written and re-read):
+//   lora_fwd:   y[M, N]  = x[M, K] w[N, K]^T + xa[M, K2] bb[N, K2]^T
+//               (xa = x A^T and bb = s Bbd, both zero-padded to K2 = 128 columns)
+//   lora_dgrad: dx[M, K] = g[M, N] w[N, K] + gb[M, K2] a[r2, K]
+//               (gb = s g Bbd zero-padded to K2 columns; a = the stacked A, r2 <= K2 valid rows)
+Tensor lora_fwd(Tensor x, Tensor w, Tensor xa, Tensor bb) {
+  for (auto* t : {&x, &w, &xa, &bb}) check_gemm_operand(*t, "lora_fwd operand");
+  const int M = x.size(0), N = w.size(0), K = x.size(1), K2 = xa.size(1);
+  TORCH_CHECK(w.size(1) == K && xa.size(0) == M && bb.size(0) == N && bb.size(1) == K2,
+              "lora_fwd: x [M,K], w [N,K], xa [M,K2], bb [N,K2]");
+  auto out = torch::empty({M, N}, x.options());
+  bcfl::G8Params g{x.data_ptr(), w.data_ptr(), out.data_ptr(), x.stride(0), w.stride(0), N, M, N, K};
+  g.kc = K;
+  g.bm = bcfl::g8_auto_bm(M, N, 1);
+  g.A2 = xa.data_ptr();
+  g.B2 = bb.data_ptr();
+  g.lda2 = xa.stride(0);
+  g.ldb2 = bb.stride(0);
+  g.K2 = K2;
+  g.K2rows = K2;
+  check_rc(bcfl::launch_g8(g, stream()), "lora_fwd");
+  return out;
+}
+
+Tensor lora_dgrad(Tensor g_, Tensor w, Tensor gb, Tensor a) {
+  for (auto* t : {&g_, &w, &gb, &a}) check_gemm_operand(*t, "lora_dgrad operand");
+  const int M = g_.size(0), N = w.size(0), K = w.size(1), K2 = gb.size(1), R = a.size(0);
+  TORCH_CHECK(g_.size(1) == N && gb.size(0) == M && a.size(1) == K && R <= K2,
+              "lora_dgrad: g [M,N], w [N,K], gb [M,K2], a [R<=K2,K]");
+  auto out = torch::empty({M, K}, g_.options());
+  bcfl::G8Params g{g_.data_ptr(), w.data_ptr(), out.data_ptr(), g_.stride(0), w.stride(0), K, M, K, N};
+  g.b_col = 1;
+  g.kc = N;
+  g.bm = bcfl::g8_auto_bm(M, K, 1);
+  g.A2 = gb.data_ptr();
+  g.B2 = a.data_ptr();
+  g.lda2 = gb.stride(0);
+  g.ldb2 = a.stride(0);
+  g.K2 = K2;
+  g.K2rows = R;
+  check_rc(bcfl::launch_g8(g, stream()), "lora_dgrad");
+  return out;
+}
+
+// whether lora_fwd (nn = false: M, N outputs, K) / lora_dgrad (nn = true) take a shape
+bool lora_native_ok(int64_t M, int64_t N, int64_t K, bool nn) {
+  bcfl::G8Params g{nullptr, nullptr, nullptr, 8, 8, 8, (int)M, (int)N, (int)K};
+  g.b_col = nn;
+  g.kc = (int)K;
+  g.bm = bcfl::g8_auto_bm((int)M, (int)N, 1);
+  g.A2 = g.B2 = reinterpret_cast<const void*>(16);
+  g.lda2 = g.ldb2 = 128;
+  g.K2 = 128;
+  g.K2rows = 64;
+  return bcfl::g8_supported(g) == 0;
+}
+
 // whether linear_fwd / linear_dgrad(_acc) take a shape (M rows, N outputs, K reduction)
 bool gemm_native_ok(int64_t M, int64_t N, int64_t K, bool nn, bool accum) {
   bcfl::G8Params g{nullptr, nullptr, nullptr, 8, 8, 8, (int)M, (int)N, (int)K};
@@ -818,6 +876,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_wgrad_kernel", &set_wgrad_kernel);
   m.def("linear_dgrad_acc", &linear_dgrad_acc);
   m.def("linear_fwd_acc", &linear_fwd_acc);
+  m.def("lora_fwd", &lora_fwd);
+  m.def("lora_dgrad", &lora_dgrad);
+  m.def("lora_native_ok", &lora_native_ok);
   m.def("gemm_native_ok", &gemm_native_ok);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("cu"), py::arg("max_s"), py::arg("nh"),
         py::arg("nkv"), py::arg("d"), py::arg("scale"), py::arg("causal"), py::arg("p8"),

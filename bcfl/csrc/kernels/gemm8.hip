@@ -89,12 +89,21 @@ struct G8Lane {
 // DMA: half-tile h of K-tile kt -> LDS byte base `dst`. ROW: idx = j*512 + tid -> row idx >> 3,
 // LDS chunk idx & 7 holds source chunk (idx & 7) ^ ((row >> 1) & 7). COL (128 idx per k-row):
 // k-row idx >> 4, LDS chunk idx & 15 holds source chunk (idx & 15) ^ colswz(k-row).
-template <bool COL, int H>
+// TAIL: a second reduction segment (K-tiles kt >= kt0 come from another matrix of the same kind,
+// e.g. the LoRA factors appended to the base projection's reduction: C = A B + A2 B2).
+template <bool COL, int H, bool TAIL = false>
 struct G8Op {
   static constexpr int L = H / 64;
   __amdgpu_buffer_rsrc_t rs;
-  int voff[2][L];  // per half: per-thread source byte offsets (k-tile 0)
+  int voff[2][L];  // per half: per-thread source byte offsets (k-tile 0 of the segment)
   int kbytes;      // source bytes per K-tile
+  // tail segment (TAIL): its operand is set up in place of the base segment's when the first
+  // K-tile >= kt0 is issued (per operand the issue order is non-decreasing in K-tile: A_hi(t + 1),
+  // A_lo(t + 2), A_hi(t + 2), ...), so it costs no extra VGPRs in the pipelined loop
+  const bf16_t* base2;
+  int64_t ld2;
+  int i02, nv2, ke2, kt0, ktb;
+  int tid_;
 
   // ROW: base = rows [i0, i0 + n_rows) of a [*, ld] matrix, K range starts at k0 (elements)
   // COL: base = k-rows [k0, k_end) of a [*, ld] matrix, columns from i0
@@ -125,9 +134,31 @@ struct G8Op {
           voff[h][j] = (int)((int64_t)r * ld * 2) + (i0 + h * H + c * 8) * 2;
         }
     }
+    if constexpr (TAIL) ktb = 0;
+  }
+  // the tail segment: K-tiles [ktiles0, ...) read `base` from its k 0 (COL: k-rows [0, k_end),
+  // rows past k_end zero-filled by the range check; ROW: zero-padded columns)
+  __device__ __forceinline__ void init2(const bf16_t* base, int64_t ld, int i0, int n_valid,
+                                        int k_end, int tid, int ktiles0) {
+    if constexpr (TAIL) {
+      base2 = base;
+      ld2 = ld;
+      i02 = i0;
+      nv2 = n_valid;
+      ke2 = k_end;
+      kt0 = ktiles0;
+      tid_ = tid;
+    }
   }
   // issue the DMA of half-tile h of K-tile kt into LDS byte offset dst (wave w's 1-KiB pieces)
-  __device__ __forceinline__ void dma(char* smem, int dst, int h, int kt, int w) const {
+  __device__ __forceinline__ void dma(char* smem, int dst, int h, int kt, int w) {
+    if constexpr (TAIL) {
+      if (kt >= kt0 && ktb == 0) {  // workgroup-uniform, once per tile
+        init(base2, ld2, i02, nv2, 0, ke2, tid_);
+        ktb = kt0;
+      }
+      kt -= ktb;
+    }
     // the K-tile offset goes into the per-lane offset (VGPR): the range check, which zero-fills
     // k-rows past the split end, covers it
     const int ko = kt * kbytes;
@@ -189,7 +220,7 @@ __device__ __forceinline__ void g8_fence(bf16x8_t (&f)[N][2]) {
     for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(f[i][s]));
 }
 
-template <int BM, bool ACOL, bool BCOL, int EPI, int ACT, bool PERSIST>
+template <int BM, bool ACOL, bool BCOL, int EPI, int ACT, bool PERSIST, bool TAIL = false>
 __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   using C = G8<BM, ACOL, BCOL, EPI, ACT>;
   constexpr int TI = C::TI, TJ = C::TJ, QM = C::QM, QN = C::QN, HA = C::HA, HB = C::HB;
@@ -226,6 +257,7 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     c.kbeg = c.split * p.kc;
     c.kend = min(p.K, c.kbeg + p.kc);
     c.nt = ((c.kend - c.kbeg + 127) / 128) * 2;  // K-tiles, even
+    if constexpr (TAIL) c.nt += p.K2 / 64;        // + the tail segment's (K2 % 128 == 0)
     return c;
   };
   TileC cur = coords(jt);
@@ -236,8 +268,8 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   const int wr = w >> 2, wc = w & 3;
 
   // ---- operands ---------------------------------------------------------------------------
-  G8Op<ACOL, HA> opA;
-  G8Op<BCOL, HB> opB;
+  G8Op<ACOL, HA, TAIL> opA;
+  G8Op<BCOL, HB, TAIL> opB;
   const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
   const bf16_t* B = reinterpret_cast<const bf16_t*>(p.B);
   auto init_ops = [&](const TileC& c) {
@@ -245,6 +277,15 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     else opA.init(A, p.lda, c.m0, 0, c.kbeg, c.kend, tid);
     if constexpr (!BCOL) opB.init(B, p.ldb, c.n0, min(BN8, p.N - c.n0), c.kbeg, c.kend, tid);
     else opB.init(B, p.ldb, c.n0, 0, c.kbeg, c.kend, tid);
+    if constexpr (TAIL) {  // splits == 1: the base segment is K-tiles [0, K / 64)
+      static_assert(!ACOL, "tail segment: ROW A operand only");
+      const int kt0 = p.K / 64;
+      opA.init2(reinterpret_cast<const bf16_t*>(p.A2), p.lda2, c.m0, min(BM, p.M - c.m0), p.K2, tid, kt0);
+      if constexpr (!BCOL)
+        opB.init2(reinterpret_cast<const bf16_t*>(p.B2), p.ldb2, c.n0, min(BN8, p.N - c.n0), p.K2, tid, kt0);
+      else
+        opB.init2(reinterpret_cast<const bf16_t*>(p.B2), p.ldb2, c.n0, 0, p.K2rows, tid, kt0);
+    }
   };
   init_ops(cur);
 
@@ -598,11 +639,34 @@ int g8_dispatch_t(const G8Params& p, hipStream_t s, int nwg) {
   return 0;
 }
 
+// tail-segment launches (EPI_STORE only: the LoRA base + low-rank products of _LoRALinear)
+template <int BM, bool BCOL, bool PERSIST>
+int g8_dispatch_tail(const G8Params& p, hipStream_t s, int nwg) {
+  if (p.epi != EPI_STORE) return -4;
+  constexpr int SLAB = T8 / 64 * G8<BM, false, BCOL, 0, 0>::QM * (G8<BM, false, BCOL, 0, 0>::QN + 4) * 4;
+  constexpr size_t lds = G8<BM, false, BCOL, 0, 0>::LDS + (PERSIST ? SLAB : 0);
+  const dim3 grid(PERSIST ? 256 : nwg), block(T8);
+  hipLaunchKernelGGL((g8_kernel<BM, false, BCOL, EPI_STORE, 0, PERSIST, true>), grid, block, lds, s, p);
+  return 0;
+}
+
 template <int BM, bool ACOL, bool BCOL>
 int g8_dispatch(const G8Params& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN8) * p.splits;
   bool persist = g8_persist_default;
   if (const char* e = std::getenv("BCFL_G8_PERSIST")) persist = e[0] == '1';
+  if constexpr (!ACOL) {
+    static const bool force_tail = [] {  // diagnostic: plain STORE GEMMs on the tail kernel
+      const char* e = std::getenv("BCFL_G8_TAIL_FORCE");
+      return e && e[0] == '1';
+    }();
+    if (p.K2 > 0 || (force_tail && p.epi == EPI_STORE && p.splits == 1)) {
+      if constexpr (BM == 128) {
+        if (persist && nwg > 256) return g8_dispatch_tail<BM, BCOL, true>(p, s, nwg);
+      }
+      return g8_dispatch_tail<BM, BCOL, false>(p, s, nwg);
+    }
+  }
   if constexpr (BM == 128) {
     if (persist && nwg > 256) return g8_dispatch_t<BM, ACOL, BCOL, true>(p, s, nwg);
   }
@@ -685,6 +749,11 @@ int g8_supported(const G8Params& p) {
   if (p.lda % 8 || p.ldb % 8 || p.ldc % 8) return -2;
   if ((p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) && (!p.aux || p.ldaux % 8)) return -3;
   if (p.epi == EPI_PARTIAL && !p.part) return -3;
+  if (p.K2 > 0) {  // tail segment: one split, ROW A2, K2 a whole number of K-tile pairs
+    if (p.a_col || p.splits != 1 || p.K2 % 128 || !p.A2 || !p.B2 || p.lda2 % 8 || p.ldb2 % 8) return -3;
+    if (p.epi != EPI_STORE) return -4;
+    if (p.b_col && (p.K2rows <= 0 || p.K2rows > p.K2)) return -3;
+  }
   return 0;
 }
 

@@ -150,6 +150,13 @@ struct G8Params {
   float* part = nullptr;         // EPI_PARTIAL: fp32 [splits, M, ldc]
   int splits = 1;
   int kc = 0;                    // reduction elements per split (multiple of 128 for ROW operands)
+  // optional tail segment of the reduction (splits == 1, ROW A, EPI_STORE): C = A B + A2 B2 with
+  // A2 / B2 of the same kinds as A / B and K2 (a multiple of 128) more reduction elements. ROW
+  // tails are zero-padded to K2 columns; a COL B2 has K2rows valid k-rows (the rest read as 0).
+  const void* A2 = nullptr;
+  const void* B2 = nullptr;
+  int64_t lda2 = 0, ldb2 = 0;
+  int K2 = 0, K2rows = 0;
 };
 int g8_supported(const G8Params& p);  // 0 = launchable
 int g8_auto_bm(int M, int N, int splits);

@@ -294,28 +294,58 @@ class _LinearAfterAct(torch.autograd.Function):
         return None, dpre, dw, None
 
 
+def _lora_k2(nr: int) -> int:
+    """Low-rank columns appended to the base reduction, padded to whole 128-deep K-tile pairs."""
+    return -(-nr // 128) * 128
+
+
+# BCFL_LORA_TAIL=1 routes _LoRALinear through the tail-segment GEMMs. Off by default: numerics
+# match fp32 (tests/test_gpu_kernels.py) but the tail-kernel build runs 3-4x slower than the base
+# kernel + low-rank GEMM pair at the Llama shapes (scripts/lora_tail_bench.py), under diagnosis.
+_LORA_TAIL = os.environ.get("BCFL_LORA_TAIL", "0") == "1"
+
+
+def _lora_tail_ok(m: int, n: int, k: int, nn_: bool, *ts: torch.Tensor) -> bool:
+    if not (_LORA_TAIL and _GEMM_PLAIN_NATIVE and all(t.dtype == torch.bfloat16 and t.stride(-1) == 1
+                                       and t.stride(0) % 8 == 0 for t in ts)):
+        return False
+    return bool(native().lora_native_ok(m, n, k, nn_))
+
+
 class _LoRALinear(torch.autograd.Function):
     """y = x W^T + s (x A^T) Bbd^T for a FROZEN base W and LoRA adapters (A stacked [n r, K], one
     B_i [o_i, r] per output block i; Bbd = block-diagonal [N, n r]).
 
-    Forward: ONE low-rank GEMM writes (s xa) Bbd^T into the output buffer, then the base GEMM
-    accumulates into it in place (beta = 1) — no cat / scale / add passes over [T, N].
-    Backward: dx = g W + s (g Bbd) A with the second product accumulated in place into the first;
+    GPU: the low-rank product rides on the base GEMM as a TAIL segment of its reduction (gemm8.hip,
+    ``lora_fwd`` / ``lora_dgrad``): y = [x | xa] [W | s Bbd]^T and dx = [g | s g Bbd] [W ; A], with
+    the n r low-rank columns zero-padded to 128 — no [M, N] delta is written and re-read and no
+    [M, K] input gradient is read-modified-written by a second GEMM. Elsewhere (or shapes the
+    kernel does not take): the low-rank GEMM writes the output and the base GEMM accumulates.
     dA = s (g Bbd)^T x; dB_i = s g_i^T xa_i (block-diagonal of one [N, n r] GEMM)."""
 
     @staticmethod
     def forward(ctx, x, w, a, s, sizes, *bs):
         x2 = x.reshape(-1, x.shape[-1])
-        xa = x2 @ a.t()                                   # [M, n r]
-        bbd = torch.block_diag(*bs)                       # [N, n r]
-        y = torch.mm(xa * s, bbd.t())                     # scale on the [M, n r] side
         if x2.stride(-1) != 1 or x2.stride(0) % 8:
             x2 = x2.contiguous()
-        if w.is_contiguous() and _native_accum_ok(x2.shape[0], w.shape[0], w.shape[1], False,
-                                                   x2, w, y):
-            native().linear_fwd_acc(x2, w, y)             # base GEMM accumulates in its epilogue
+        M, N, K = x2.shape[0], w.shape[0], w.shape[1]
+        nr = a.shape[0]
+        bbd = torch.block_diag(*bs)                       # [N, n r]
+        if w.is_contiguous() and _lora_tail_ok(M, N, K, False, x2, w):
+            k2 = _lora_k2(nr)
+            xa_p = x2.new_zeros(M, k2)
+            torch.mm(x2, a.t(), out=xa_p[:, :nr])         # [M, n r] into the padded tail operand
+            bb_p = w.new_zeros(N, k2)
+            torch.mul(bbd, s, out=bb_p[:, :nr])
+            y = native().lora_fwd(x2, w, xa_p, bb_p)
+            xa = xa_p[:, :nr]
         else:
-            y.addmm_(x2, w.t())
+            xa = x2 @ a.t()                               # [M, n r]
+            y = torch.mm(xa * s, bbd.t())                 # scale on the [M, n r] side
+            if w.is_contiguous() and _native_accum_ok(M, N, K, False, x2, w, y):
+                native().linear_fwd_acc(x2, w, y)         # base GEMM accumulates in its epilogue
+            else:
+                y.addmm_(x2, w.t())
         ctx.save_for_backward(x2, w, a, xa, bbd)
         ctx.s, ctx.sizes, ctx.xshape = s, sizes, x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -325,11 +355,20 @@ class _LoRALinear(torch.autograd.Function):
         x2, w, a, xa, bbd = ctx.saved_tensors
         s, sizes = ctx.s, ctx.sizes
         g2 = g.reshape(-1, w.shape[0])
+        if g2.stride(-1) != 1 or g2.stride(0) % 8:
+            g2 = g2.contiguous()
+        M, N, K = g2.shape[0], w.shape[0], w.shape[1]
+        nr = a.shape[0]
         gb = g2 @ bbd                                     # [M, n r]
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_gemm(g2, w) if w.is_contiguous() else g2 @ w
-            dx.addmm_(gb, a, alpha=s)                     # LoRA input gradient, in place
+            if w.is_contiguous() and _lora_tail_ok(M, K, N, True, g2, w, a):
+                gb_p = g2.new_zeros(M, _lora_k2(nr))
+                torch.mul(gb, s, out=gb_p[:, :nr])
+                dx = native().lora_dgrad(g2, w, gb_p, a)  # g W + (s g Bbd) A in one GEMM
+            else:
+                dx = _dgrad_gemm(g2, w) if w.is_contiguous() else g2 @ w
+                dx.addmm_(gb, a, alpha=s)                 # LoRA input gradient, in place
             dx = dx.view(ctx.xshape)
         # tall-skinny reductions over the M tokens: at the LoRA step's M (~2k tokens) the library
         # beats the 8-phase weight-gradient kernel with a zero-padded 256-column operand

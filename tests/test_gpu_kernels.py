@@ -565,6 +565,37 @@ def test_lora_linear_fused_matches_unfused(T):
         assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("M,N,K,nr", [(1000, 768, 512, 48), (7680, 3072, 768, 48),
+                                       (2048, 512, 1024, 16), (512, 256, 256, 160)])
+def test_lora_tail_gemms_match_fp32(M, N, K, nr):
+    """gemm8.hip tail segment: lora_fwd = x W^T + xa bb^T and lora_dgrad = g W + gb A in ONE
+    GEMM (low-rank columns zero-padded to whole 128-deep K-tile pairs; the COL A operand's rows
+    past nr read as zero), vs fp32 torch. Covers BM 256 / 128, the persistent grid (7680 x 3072)
+    and a tail of two K-tile pairs (nr = 160)."""
+    torch.manual_seed(M + N + nr)
+    C = ops.native()
+    k2 = -(-nr // 128) * 128
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    xa = torch.zeros(M, k2, device=DEV, dtype=torch.bfloat16)
+    xa[:, :nr] = torch.randn(M, nr, device=DEV).bfloat16()
+    bb = torch.zeros(N, k2, device=DEV, dtype=torch.bfloat16)
+    bb[:, :nr] = (torch.randn(N, nr, device=DEV) * 0.1).bfloat16()
+    assert C.lora_native_ok(M, N, K, False)
+    y = C.lora_fwd(x, w, xa, bb)
+    ref_y = x.float() @ w.float().t() + xa.float() @ bb.float().t()
+    _close(y, ref_y, 5e-2, 2e-2)
+    g = torch.randn(M, N, device=DEV).bfloat16()
+    gb = torch.zeros(M, k2, device=DEV, dtype=torch.bfloat16)
+    gb[:, :nr] = torch.randn(M, nr, device=DEV).bfloat16()
+    gb[:, nr:] = 7.0  # padding columns are ignored: the A operand's rows past nr read as zero
+    a = (torch.randn(nr, K, device=DEV) * 0.1).bfloat16()
+    assert C.lora_native_ok(M, K, N, True)
+    dx = C.lora_dgrad(g, w, gb, a)
+    ref_dx = g.float() @ w.float() + gb[:, :nr].float() @ a.float()
+    _close(dx, ref_dx, 5e-2, 2e-2)
+
+
 @pytest.mark.parametrize("B,C", [(32, 2), (7, 41), (256, 40), (300, 3)])
 def test_xent_kernels_match_torch(B, C):
     torch.manual_seed(B + C)
