@@ -1,5 +1,6 @@
-"""Diagnostic: the 8-phase GEMM's tail-segment kernel vs the base kernel at a Llama shape
-(run with BCFL_G8_TAIL_FORCE=0 / 1: plain STORE GEMMs on the base / tail kernel)."""
+"""Diagnostic: the 8-phase GEMM's tail-segment kernel vs the base kernel at Llama shapes, with
+zero and random tail operands, interleaved in one process (BCFL_G8_TAIL_FORCE=1 runs the plain
+STORE GEMMs on the tail kernel too)."""
 import os
 import sys
 
@@ -9,11 +10,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bcfl import ops  # noqa: E402
 
 C = ops.native()
-M, N, K = 8192, 6144, 4096
-x = torch.randn(M, K, device="cuda").bfloat16()
-w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
-xa = torch.zeros(M, 128, device="cuda", dtype=torch.bfloat16)
-bb = torch.zeros(N, 128, device="cuda", dtype=torch.bfloat16)
 
 
 def t(fn, reps=10):
@@ -28,5 +24,26 @@ def t(fn, reps=10):
     return round(e0.elapsed_time(e1) / reps * 1e3, 1)
 
 
-print("force", os.environ.get("BCFL_G8_TAIL_FORCE"), "linear_fwd_us", t(lambda: C.linear_fwd(x, w, None, -1)),
-      "lora_fwd_us", t(lambda: C.lora_fwd(x, w, xa, bb)), flush=True)
+M = 8192
+for name, N, K, nr in (("qkv", 6144, 4096, 48), ("gate_up", 28672, 4096, 32)):
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    xz = torch.zeros(M, 128, device="cuda", dtype=torch.bfloat16)
+    bz = torch.zeros(N, 128, device="cuda", dtype=torch.bfloat16)
+    xr, br = xz.clone(), bz.clone()
+    xr[:, :nr] = torch.randn(M, nr, device="cuda").bfloat16()
+    br[:, :nr] = (torch.randn(N, nr, device="cuda") * 0.02).bfloat16()
+    g = torch.randn(M, N, device="cuda").bfloat16()
+    a = (torch.randn(nr, K, device="cuda") * 0.02).bfloat16()
+    gz = torch.zeros(M, 128, device="cuda", dtype=torch.bfloat16)
+    gr = gz.clone()
+    gr[:, :nr] = torch.randn(M, nr, device="cuda").bfloat16()
+    for rep in range(2):
+        print(name, "rep", rep, "force", os.environ.get("BCFL_G8_TAIL_FORCE"),
+              "fwd", t(lambda: C.linear_fwd(x, w, None, -1)),
+              "lora_fwd0", t(lambda: C.lora_fwd(x, w, xz, bz)),
+              "lora_fwdR", t(lambda: C.lora_fwd(x, w, xr, br)),
+              "dgrad", t(lambda: C.linear_dgrad(g, w, None, -1)),
+              "lora_dgrad0", t(lambda: C.lora_dgrad(g, w, gz, a)),
+              "lora_dgradR", t(lambda: C.lora_dgrad(g, w, gr, a)), flush=True)
