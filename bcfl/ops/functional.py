@@ -299,10 +299,10 @@ def _lora_k2(nr: int) -> int:
     return -(-nr // 128) * 128
 
 
-# BCFL_LORA_TAIL=1 routes _LoRALinear through the tail-segment GEMMs. Off by default: numerics
-# match fp32 (tests/test_gpu_kernels.py) but the tail-kernel build runs 3-4x slower than the base
-# kernel + low-rank GEMM pair at the Llama shapes (scripts/lora_tail_bench.py), under diagnosis.
-_LORA_TAIL = os.environ.get("BCFL_LORA_TAIL", "0") == "1"
+# _LoRALinear on the tail-segment GEMMs (BCFL_LORA_TAIL=0: the two-GEMM path). At the Llama-3-8B
+# shapes (M = 8192) the fused GEMM costs the base GEMM + 1-3 % (scripts/tail_diag.py) and config 5
+# goes 17.05 -> 16.53 s/round (profiles/lora_tail_r3.json)
+_LORA_TAIL = os.environ.get("BCFL_LORA_TAIL", "1") == "1"
 
 
 def _lora_tail_ok(m: int, n: int, k: int, nn_: bool, *ts: torch.Tensor) -> bool:
