@@ -393,7 +393,9 @@ std::vector<Tensor> rmsnorm_bwd(Tensor dout, Tensor x, Tensor w, Tensor rstd, bo
   const int H = x.size(-1);
   const int T = x.numel() / H;
   auto dx = torch::empty_like(x);
-  const int nblk = bcfl::bwd_blocks(T);
+  // with a weight gradient: a few rows per wave (per-block dw partials, then one colsum pass);
+  // frozen weight (LoRA): one row per wave, every row's loads in flight at once
+  const int nblk = need_dw ? bcfl::bwd_blocks(T) : (T + 3) / 4;
   Tensor partial;
   if (need_dw) partial = torch::empty({nblk, H}, x.options().dtype(torch::kFloat));
   check_rc(bcfl::launch_rmsnorm_bwd(dout.data_ptr(), x.data_ptr(), w.data_ptr(),

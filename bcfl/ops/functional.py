@@ -312,16 +312,41 @@ def _lora_tail_ok(m: int, n: int, k: int, nn_: bool, *ts: torch.Tensor) -> bool:
     return bool(native().lora_native_ok(m, n, k, nn_))
 
 
+_EPI_PARTIAL = 5  # gemm8.hip fp32 split-K partials
+# BCFL_LORA_G8=0: the fused LoRA path keeps its tail segments but computes the four tall-skinny
+# low-rank products with the library (A/B of profiles/lora_tail_r3.json)
+_LORA_G8_SKINNY = os.environ.get("BCFL_LORA_G8", "1") == "1"
+_LORA_PAD = 256   # the low-rank dimension padded to one 8-phase GEMM column tile
+
+
+def _g8_skinny(A: torch.Tensor, B: torch.Tensor, b_col: bool, ways: int = 4) -> torch.Tensor:
+    """C[M, 256] = A[M, K] B (B ROW [256, K] or COL [K, 256]) on the 8-phase GEMM with the reduction
+    split ``ways`` ways (a 256-column output alone gives M / 128 workgroups, a quarter of the chip
+    at M = 8k); the fp32 slice partials are summed in one pass."""
+    K = A.shape[1]
+    kc = -(-K // (ways * 128)) * 128
+    n = -(-K // kc)
+    if n == 1:
+        return native().gemm8(A, B, False, b_col, 0, 0, None, None, None, 0, 1, 0)[0]
+    part = native().gemm8(A, B, False, b_col, _EPI_PARTIAL, 0, None, None, None, 0, n, kc)[0]
+    return part.sum(0).to(A.dtype)
+
+
 class _LoRALinear(torch.autograd.Function):
     """y = x W^T + s (x A^T) Bbd^T for a FROZEN base W and LoRA adapters (A stacked [n r, K], one
     B_i [o_i, r] per output block i; Bbd = block-diagonal [N, n r]).
 
-    GPU: the low-rank product rides on the base GEMM as a TAIL segment of its reduction (gemm8.hip,
-    ``lora_fwd`` / ``lora_dgrad``): y = [x | xa] [W | s Bbd]^T and dx = [g | s g Bbd] [W ; A], with
-    the n r low-rank columns zero-padded to 128 — no [M, N] delta is written and re-read and no
-    [M, K] input gradient is read-modified-written by a second GEMM. Elsewhere (or shapes the
-    kernel does not take): the low-rank GEMM writes the output and the base GEMM accumulates.
-    dA = s (g Bbd)^T x; dB_i = s g_i^T xa_i (block-diagonal of one [N, n r] GEMM)."""
+    GPU (M >= 1024 tokens): every product is an 8-phase MFMA GEMM (gemm8.hip), the low-rank
+    dimension n r zero-padded to one 256-column tile:
+      xa  = x A_pad^T                      (split-K, [M, 256], columns >= n r are zero)
+      y   = [x | xa] [W | s Bbd_pad]^T     (the low-rank product as a TAIL segment of the base
+                                            GEMM's reduction: no [M, N] delta written / re-read)
+      gbs = g (s Bbd_pad)                  (split-K, [M, 256])
+      dx  = [g | gbs] [W ; A]              (tail segment again)
+      dA  = gbs^T x,  dB = s g^T xa        (weight-gradient kernel, 256 tile slots)
+    The library's tall-skinny kernels reduce M = 8k tokens in a handful of workgroups (16.9 % of
+    config 5's kernel time, profiles/config5_kernel_stats_r3.md). Elsewhere (CPU, small M, other
+    shapes): the low-rank GEMM writes the output and the base GEMM accumulates in place."""
 
     @staticmethod
     def forward(ctx, x, w, a, s, sizes, *bs):
@@ -331,14 +356,23 @@ class _LoRALinear(torch.autograd.Function):
         M, N, K = x2.shape[0], w.shape[0], w.shape[1]
         nr = a.shape[0]
         bbd = torch.block_diag(*bs)                       # [N, n r]
-        if w.is_contiguous() and _lora_tail_ok(M, N, K, False, x2, w):
+        fused = (w.is_contiguous() and a.is_contiguous() and nr <= _LORA_PAD and M >= WGRAD_MIN_ROWS
+                 and N % 256 == 0 and K % 256 == 0
+                 and _lora_tail_ok(M, N, K, False, x2, w) and _lora_tail_ok(M, K, N, True, x2, w))
+        ctx.fused = fused
+        if fused:
             k2 = _lora_k2(nr)
-            xa_p = x2.new_zeros(M, k2)
-            torch.mm(x2, a.t(), out=xa_p[:, :nr])         # [M, n r] into the padded tail operand
-            bb_p = w.new_zeros(N, k2)
+            if _LORA_G8_SKINNY:
+                a_p = a.new_zeros(_LORA_PAD, K)
+                a_p[:nr] = a
+                xa_f = _g8_skinny(x2, a_p, False)         # [M, 256]
+            else:
+                xa_f = x2.new_zeros(M, _LORA_PAD)
+                torch.mm(x2, a.t(), out=xa_f[:, :nr])
+            bb_p = w.new_zeros(N, _LORA_PAD)
             torch.mul(bbd, s, out=bb_p[:, :nr])
-            y = native().lora_fwd(x2, w, xa_p, bb_p)
-            xa = xa_p[:, :nr]
+            y = native().lora_fwd(x2, w, xa_f[:, :k2], bb_p[:, :k2])
+            ctx.save_for_backward(x2, w, a, xa_f, bb_p)
         else:
             xa = x2 @ a.t()                               # [M, n r]
             y = torch.mm(xa * s, bbd.t())                 # scale on the [M, n r] side
@@ -346,35 +380,47 @@ class _LoRALinear(torch.autograd.Function):
                 native().linear_fwd_acc(x2, w, y)         # base GEMM accumulates in its epilogue
             else:
                 y.addmm_(x2, w.t())
-        ctx.save_for_backward(x2, w, a, xa, bbd)
+            ctx.save_for_backward(x2, w, a, xa, bbd)
         ctx.s, ctx.sizes, ctx.xshape = s, sizes, x.shape
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, g):
-        x2, w, a, xa, bbd = ctx.saved_tensors
         s, sizes = ctx.s, ctx.sizes
-        g2 = g.reshape(-1, w.shape[0])
+        g2 = g.reshape(-1, g.shape[-1])
         if g2.stride(-1) != 1 or g2.stride(0) % 8:
             g2 = g2.contiguous()
-        M, N, K = g2.shape[0], w.shape[0], w.shape[1]
-        nr = a.shape[0]
-        gb = g2 @ bbd                                     # [M, n r]
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if w.is_contiguous() and _lora_tail_ok(M, K, N, True, g2, w, a):
-                gb_p = g2.new_zeros(M, _lora_k2(nr))
-                torch.mul(gb, s, out=gb_p[:, :nr])
-                dx = native().lora_dgrad(g2, w, gb_p, a)  # g W + (s g Bbd) A in one GEMM
-            else:
-                dx = _dgrad_gemm(g2, w) if w.is_contiguous() else g2 @ w
-                dx.addmm_(gb, a, alpha=s)                 # LoRA input gradient, in place
-            dx = dx.view(ctx.xshape)
-        # tall-skinny reductions over the M tokens: at the LoRA step's M (~2k tokens) the library
-        # beats the 8-phase weight-gradient kernel with a zero-padded 256-column operand
-        # (config 5 kernel stats: 2.8 s -> 9.9 s of kernel time per 3 rounds, reverted)
-        da = (gb.t() @ x2).mul_(s) if ctx.needs_input_grad[2] else None
+        dx = da = None
         dbs = [None] * len(sizes)
+        if ctx.fused:
+            x2, w, a, xa_f, bb_p = ctx.saved_tensors
+            nr = a.shape[0]
+            if _LORA_G8_SKINNY:
+                gbs = _g8_skinny(g2, bb_p, True)          # [M, 256] = g (s Bbd_pad)
+            else:
+                gbs = g2.new_zeros(g2.shape[0], _LORA_PAD)
+                torch.mm(g2, bb_p[:, :nr], out=gbs[:, :nr])
+            if ctx.needs_input_grad[0]:
+                dx = native().lora_dgrad(g2, w, gbs[:, :_lora_k2(nr)], a).view(ctx.xshape)
+            if ctx.needs_input_grad[2]:
+                da = (native().wgrad(gbs, x2, 256)[:nr] if _LORA_G8_SKINNY
+                      else gbs[:, :nr].t() @ x2)          # (s g Bbd)^T x
+            if any(ctx.needs_input_grad[5:]):
+                full = (native().wgrad(g2, xa_f, 256)[:, :nr] if _LORA_G8_SKINNY
+                        else g2.t() @ xa_f[:, :nr]).mul_(s)  # [N, n r]; block i = dB_i
+                r = nr // len(sizes)
+                o = 0
+                for i, n in enumerate(sizes):
+                    dbs[i] = full[o:o + n, i * r:(i + 1) * r].contiguous()
+                    o += n
+            return (dx, None, da, None, None, *dbs)
+        x2, w, a, xa, bbd = ctx.saved_tensors
+        gb = g2 @ bbd                                     # [M, n r]
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad_gemm(g2, w) if w.is_contiguous() else g2 @ w
+            dx.addmm_(gb, a, alpha=s)                     # LoRA input gradient, in place
+            dx = dx.view(ctx.xshape)
+        da = (gb.t() @ x2).mul_(s) if ctx.needs_input_grad[2] else None
         if any(ctx.needs_input_grad[5:]):
             full = (g2.t() @ xa).mul_(s)                  # [N, n r]; block i = dB_i
             r = xa.shape[1] // len(sizes)

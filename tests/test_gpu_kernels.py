@@ -535,10 +535,12 @@ def test_native_dropout_mask_matches_hash_layout():
     _close(y, r, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("T", [1000, 2048])
+@pytest.mark.parametrize("T", [1000, 2048, 4096])
 def test_lora_linear_fused_matches_unfused(T):
-    """ops.lora_linear (low-rank product written first, frozen base GEMM accumulating in place;
-    custom backward) == the unfused x W^T + cat(xa_i B_i^T) * s path, forward and gradients."""
+    """ops.lora_linear == the unfused x W^T + cat(xa_i B_i^T) * s path, forward and gradients.
+    T = 1000: the two-GEMM path (low-rank product written first, base GEMM accumulating);
+    T >= 1024: every product on the 8-phase GEMM (split-K skinny GEMMs, tail segments, weight-
+    gradient kernel)."""
     import os
     torch.manual_seed(4)
     K, r = 512, 16
