@@ -1,7 +1,12 @@
 """Diagnose overlapped-wgrad vs inline gradient differences on one step (bert-base-2l)."""
+import os
+import sys
+
 import numpy as np
 import torch
-import bcfl  # noqa: F401
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bcfl  # noqa: F401,E402
 import bcfl.ops as ops
 from bcfl.data.batching import make_packed_batch
 from bcfl.data.registry import load_split
