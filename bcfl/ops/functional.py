@@ -513,6 +513,12 @@ class _BDALN(torch.autograd.Function):
                                                             bool(has_b))
         if has_r and ctx.tap is not None:
             ctx.tap.g, dres = dres, None   # the consumer GEMM accumulates into it
+        elif has_r and not p8 and _WG["enabled"]:
+            # without dropout the kernel returns ONE buffer as dy and dres; autograd may sum the
+            # residual's other gradient into it in place while the out-projection's side-stream
+            # weight gradient is still reading dy (caught by scripts/overlap_diag.py: layer-0
+            # attn_out / out weight gradients off by up to 17 %)
+            dres = dres.clone()
         return (dy, dbias if has_b else None, dres if has_r else None, dgamma,
                 dbeta if has_beta else None, None, None, None, None, None)
 

@@ -381,10 +381,10 @@ def test_linear_autograd_uses_wgrad_kernel():
 def test_overlapped_wgrad_matches_inline(model):
     """Side-stream weight gradients (the 8-phase kernel on a paired stream, joined before the
     optimizer) give the inline path's parameter gradients; ALBERT's shared layer opts out.
-    Tolerance, not bitwise: the embedding / layer-0 gradients carry timing-dependent fp32
-    reduction order (1e-6..1e-4 absolute, scripts/overlap_diag.py) and a strict compare failed on
-    the round-3 tree; a stream-ordering race (a side-stream kernel reading an operand before it is
-    written or after it is reused) shows up as O(1) relative error."""
+    Bitwise in practice (scripts/overlap_diag.py); compared at 1e-3 relative so a stray fp32 ULP
+    cannot fail it while a stream-ordering race cannot pass: the round-3 suite caught one (without
+    dropout the LayerNorm backward's dy and residual gradient were one buffer, summed into in place
+    while the out-projection's side-stream weight gradient still read it: 17 % error in layer 0)."""
     from bcfl.data.batching import make_packed_batch
     from bcfl.data.registry import load_split
     from bcfl.models import build_model, special_tokens
@@ -405,7 +405,7 @@ def test_overlapped_wgrad_matches_inline(model):
         finally:
             ops.set_wgrad_overlap(False)
     assert len(grads[False]) == len(grads[True])
-    _grads_close(grads[True], grads[False], tol=2e-2)
+    _grads_close(grads[True], grads[False], tol=1e-3)
 
 
 # ---------------------------------------------------------------------------------------------
