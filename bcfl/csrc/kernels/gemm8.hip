@@ -607,9 +607,9 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
 // epilogue slab) when the launch has more tiles than CUs; BCFL_G8_PERSIST=0/1 overrides.
 // Measured: BERT shapes 0-5 % per GEMM (profiles/g8_persistent_r3.json), one-client round
 // 0.0922 -> 0.0913 s, 8-lane round 0.5635 -> 0.5604 s (3 / 2 interleaved reps)
-// Off by default: the round-3 GPU suite caught test_overlapped_wgrad_matches_inline failing with it
-// on (side-stream weight gradients vs inline) and passing at the commit before it was enabled.
-bool g8_persist_default = false;
+// (The round-3 overlap-test failure first blamed on it was the dy / dres aliasing race fixed in
+// ops._BDALN: scripts/overlap_diag.py showed the same two gradients off with it on and off.)
+bool g8_persist_default = true;
 
 template <int BM, bool ACOL, bool BCOL, bool PERSIST>
 int g8_dispatch_t(const G8Params& p, hipStream_t s, int nwg) {
