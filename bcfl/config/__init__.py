@@ -70,6 +70,12 @@ class FLConfig:
     topology: str = "full"              # full | ring | pagerank (serverless neighbour graph)
     mixing: str = "average"             # average (reference mean) | metropolis
     async_gossip: bool = True           # exchange on the side stream, mix stale-by-one replicas
+    # SCAFFOLD's federation control variate c' = (x - x') / L needs x' to mix models trained in the
+    # SAME round: with drift correction on and several ranks, async posts stay concurrent and
+    # one-sided but the mix waits for every live neighbour's round-r snapshot (stale-by-one mixing
+    # shrinks c' by the stale fraction: 2 ranks on one MI355X stayed at the 0.5 majority rate after
+    # 25 rounds, profiles/multirank_learning_r3.json)
+    drift_same_round_mix: bool = True
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
                                         # (matched send/recv); auto = mailbox when async, else rccl
     verify_updates: bool = True         # receivers re-hash every received payload vs its root

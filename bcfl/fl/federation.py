@@ -172,6 +172,10 @@ class Federation:
         # ---------------- gossip -------------------------------------------------------------------
         if cfg.gossip_transport not in ("auto", "mailbox", "rccl"):
             raise ValueError(f"unknown gossip_transport {cfg.gossip_transport!r}")
+        # drift correction across ranks: mix same-round snapshots (FLConfig.drift_same_round_mix)
+        self.same_round_mix = bool(cfg.mode == "serverless" and cfg.async_gossip
+                                   and cfg.drift_same_round_mix and self.drift.enabled
+                                   and self.rt.distributed)
         self.transport = cfg.gossip_transport
         if self.transport == "auto":
             # deterministic: the lock-step engine mixes exactly the previous round's states
@@ -202,7 +206,7 @@ class Federation:
                 try:
                     self.gossip = MailboxGossip(n, states, self.nbrs,
                                                 "fp32" if cfg.wire_dtype == "fp32" else "bf16",
-                                                sync=not cfg.async_gossip,
+                                                sync=not cfg.async_gossip or self.same_round_mix,
                                                 liveness_timeout=cfg.liveness_timeout,
                                                 verify=cfg.verify_updates)
                 except MailboxUnavailable as e:
@@ -216,7 +220,8 @@ class Federation:
                 wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
                 if cfg.wire_dtype == "bf16_raw":
                     wire = "bf16"
-                self.gossip = GossipEngine(n, states, self.nbrs, wire, cfg.async_gossip,
+                self.gossip = GossipEngine(n, states, self.nbrs, wire,
+                                           cfg.async_gossip and not self.same_round_mix,
                                            liveness_timeout=cfg.liveness_timeout,
                                            verify=cfg.verify_updates)
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
@@ -1089,7 +1094,7 @@ class Federation:
         for x in recs:
             x["verdict"] = v.verdict(x["client"])
         # async mixes states published last round -> apply last round's verdicts to them
-        use_v = self.prev_verdicts if cfg.async_gossip else v
+        use_v = self.prev_verdicts if (cfg.async_gossip and not self.same_round_mix) else v
         W = mixing_matrix(self.nbrs, cfg.mixing, use_v.rejected)
         with self.timer.phase("comm"):
             pout = (self.client_param if self.lanes else

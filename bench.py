@@ -238,6 +238,9 @@ def main():
                        "parallelism": f"fl{a.clients}-clients-on-{rt.world}gpu",
                        "clients": a.clients, "mode": a.mode,
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
+                       "gossip_mix": ("same-round snapshots (drift correction across ranks)"
+                                      if getattr(fed, "same_round_mix", False) else
+                                      "newest complete snapshot" if not a.sync else "same-round"),
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
                        "client_lanes_per_gpu": len(fed.lanes) or 1,
                        "micro_batches_per_step": fed.micro_split,
