@@ -313,9 +313,11 @@ def _lora_tail_ok(m: int, n: int, k: int, nn_: bool, *ts: torch.Tensor) -> bool:
 
 
 _EPI_PARTIAL = 5  # gemm8.hip fp32 split-K partials
-# BCFL_LORA_G8=0: the fused LoRA path keeps its tail segments but computes the four tall-skinny
-# low-rank products with the library (A/B of profiles/lora_tail_r3.json)
-_LORA_G8_SKINNY = os.environ.get("BCFL_LORA_G8", "1") == "1"
+# The fused LoRA path computes the four tall-skinny low-rank products with the library by default:
+# same-box A/B at config 5 (2 lanes) 16.63 vs 17.07-17.09 s/round for the split-K 8-phase variant
+# (BCFL_LORA_G8=1) — the library's small grids co-run with the other lane's GEMMs
+# (profiles/lora_tail_r3.json)
+_LORA_G8_SKINNY = os.environ.get("BCFL_LORA_G8", "0") == "1"
 _LORA_PAD = 256   # the low-rank dimension padded to one 8-phase GEMM column tile
 
 
@@ -336,17 +338,19 @@ class _LoRALinear(torch.autograd.Function):
     """y = x W^T + s (x A^T) Bbd^T for a FROZEN base W and LoRA adapters (A stacked [n r, K], one
     B_i [o_i, r] per output block i; Bbd = block-diagonal [N, n r]).
 
-    GPU (M >= 1024 tokens): every product is an 8-phase MFMA GEMM (gemm8.hip), the low-rank
-    dimension n r zero-padded to one 256-column tile:
-      xa  = x A_pad^T                      (split-K, [M, 256], columns >= n r are zero)
+    GPU (M >= 1024 tokens), the low-rank dimension n r zero-padded to one 256-column tile:
+      xa  = x A_pad^T                      ([M, 256], columns >= n r are zero)
       y   = [x | xa] [W | s Bbd_pad]^T     (the low-rank product as a TAIL segment of the base
                                             GEMM's reduction: no [M, N] delta written / re-read)
-      gbs = g (s Bbd_pad)                  (split-K, [M, 256])
+      gbs = g (s Bbd_pad)                  ([M, 256])
       dx  = [g | gbs] [W ; A]              (tail segment again)
-      dA  = gbs^T x,  dB = s g^T xa        (weight-gradient kernel, 256 tile slots)
-    The library's tall-skinny kernels reduce M = 8k tokens in a handful of workgroups (16.9 % of
-    config 5's kernel time, profiles/config5_kernel_stats_r3.md). Elsewhere (CPU, small M, other
-    shapes): the low-rank GEMM writes the output and the base GEMM accumulates in place."""
+      dA  = gbs^T x,  dB = s g^T xa
+    The four tall-skinny products (xa, gbs, dA, dB) run on the library by default and on split-K
+    8-phase GEMMs / the weight-gradient kernel with BCFL_LORA_G8=1: the library's kernels reduce
+    M = 8k tokens in a handful of workgroups (16.9 % of config 5's kernel time,
+    profiles/config5_kernel_stats_r3.md) but co-run with the other lane's GEMMs, and measured 2.6 %
+    faster at the wall. Elsewhere (CPU, small M, other shapes): the low-rank GEMM writes the
+    output and the base GEMM accumulates in place."""
 
     @staticmethod
     def forward(ctx, x, w, a, s, sizes, *bs):
