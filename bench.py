@@ -4,8 +4,9 @@ gossip, Non-IID — BASELINE.json's metric on BASELINE.json config 3.
 
 One "step" = one federated ROUND of an 8-client federation: every client trains one local epoch
 (240 samples = 8 batches of 32, reference ``serverless_NonIID_IMDB.py:59``), evaluates on its 60
-local test rows, publishes its model into its peers' one-sided hipIpc mailboxes (async: the copy
-runs on a side stream while the next round trains; receivers mix the newest complete snapshot),
+local test rows, publishes its model into its peers' one-sided hipIpc mailboxes (async: the copies
+to every peer run concurrently on side streams; receivers mix the newest complete snapshot — with
+drift correction across ranks, the round's own snapshot, see FLConfig.drift_same_round_mix),
 every received payload is re-hashed and checked against its sender's committed Merkle root
 before it is mixed (only at N > 1: with all 8 clients on one rank nothing crosses a process),
 every client model is scored on its stride of a class-balanced 1000-row global draw (overlapped
