@@ -207,6 +207,10 @@ class Federation:
                     self.gossip = MailboxGossip(n, states, self.nbrs,
                                                 "fp32" if cfg.wire_dtype == "fp32" else "bf16",
                                                 sync=not cfg.async_gossip or self.same_round_mix,
+                                                # same-round mix: a peer whose round-r post has not
+                                                # landed within 10 s is declared dead for the mix
+                                                # (its later posts bring it back), not waited on
+                                                sync_timeout_s=10.0 if self.same_round_mix else 60.0,
                                                 liveness_timeout=cfg.liveness_timeout,
                                                 verify=cfg.verify_updates)
                 except MailboxUnavailable as e:
