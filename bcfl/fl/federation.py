@@ -165,6 +165,13 @@ class Federation:
         if cfg.deterministic:
             ov = False  # the overlapped path's gradients are not bitwise reproducible
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
+        if self.is_cuda and ops.native_available():
+            # persistent GEMM grids (one workgroup per CU walking the tiles) pay with concurrent
+            # client lanes (8-lane round 0.5635 -> 0.5604 s, profiles/g8_persistent_r3.json) and
+            # cost a rank that trains one client with side-stream weight gradients, whose 64-slot
+            # weight-gradient grid they crowd out (0.0975 vs 0.1021 s/round, 3 interleaved reps,
+            # profiles/g8_persistent_1client_r3.json); BCFL_G8_PERSIST=0/1 overrides
+            ops.native().set_g8_persistent(not bool(ov))
         self.global_master: Optional[torch.Tensor] = None
         if cfg.mode == "server":
             self.global_master = self.flat.master.detach().clone()
