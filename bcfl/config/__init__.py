@@ -96,7 +96,7 @@ class FLConfig:
                                         # 0 = auto (= off: host-bound for BERT-base, see
                                         # Federation._build_micro), 1 = off, 2 = on
     client_lanes: int = 0               # concurrent client lanes per rank (own replica + HIP stream);
-                                        # 0 = auto: min(6, hosted) on GPU (min(2, hosted) for
+                                        # 0 = auto: min(6 serverless / 8 server, hosted) on GPU (min(2, hosted) for
                                         # models > 1e9 parameters: activation memory), 1 on CPU
     # --- trust layer -------------------------------------------------------------
     anomaly_filter: str = "none"        # none | pagerank | modz | both

@@ -292,11 +292,12 @@ class Federation:
         else:
             # activation memory per lane grows with the model: an 8B-parameter client step holds
             # ~45 GB of saved activations at 11k tokens, so big models get 2 lanes (288 GB HBM;
-            # config 5: 1 / 2 / 3 / 4 lanes 18.1 / 16.6 / 19.2 / 21.8 s/round). BERT-size models
-            # get 6: with 8 clients 6 lanes beat 8 in 4 / 4 interleaved reps (0.548 vs 0.560 s/round,
-            # profiles/lanes_count_ab_r3.json; the box runs 4 hardware queues per process)
+            # config 5: 1 / 2 / 3 / 4 lanes 18.1 / 16.6 / 19.2 / 21.8 s/round). BERT-size models:
+            # serverless 6 (8 clients: 6 lanes beat 8 in 4 / 4 interleaved reps, 0.548 vs 0.560
+            # s/round; the box runs 4 hardware queues per process), server 8 (config 2, 4 steps per
+            # client: 8 lanes beat 6, 0.338-0.345 vs 0.374-0.380; profiles/lanes_count_ab_r3.json)
             big = sum(p.numel() for p in self.model.parameters()) > 1_000_000_000
-            n = min(2 if big else 6, len(self.local_clients))
+            n = min(2 if big else (8 if cfg.mode == "server" else 6), len(self.local_clients))
         n = max(1, min(n, len(self.local_clients)))
         lanes = []
         for i in range(n):
