@@ -58,6 +58,8 @@ class FLConfig:
     adam_eps: float = 1e-6
     adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
     keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
+    max_grad_norm: float = 0.0          # global-norm gradient clipping per local step (0 = off:
+                                        # the reference's plain loop); fused into the AdamW pass
     drift_correction: str = "none"      # none | scaffold | auto (control variates in update
                                         # space, fused into AdamW; no extra communication —
                                         # fl/drift.py). auto = scaffold for label-skewed
@@ -70,12 +72,21 @@ class FLConfig:
     topology: str = "full"              # full | ring | pagerank (serverless neighbour graph)
     mixing: str = "average"             # average (reference mean) | metropolis
     async_gossip: bool = True           # exchange on the side stream, mix stale-by-one replicas
-    # SCAFFOLD's federation control variate c' = (x - x') / L needs x' to mix models trained in the
-    # SAME round: with drift correction on and several ranks, async posts stay concurrent and
-    # one-sided but the mix waits for every live neighbour's round-r snapshot (stale-by-one mixing
-    # shrinks c' by the stale fraction: 2 ranks on one MI355X stayed at the 0.5 majority rate after
-    # 25 rounds, profiles/multirank_learning_r3.json)
-    drift_same_round_mix: bool = True
+    # Drift correction across ranks with async mailbox gossip: every client publishes its SCAFFOLD
+    # control variate with its model (one payload, one version) and the federation control variate
+    # is formed from the neighbours' newest snapshots, whatever their round (fl/drift.py, exchange
+    # mode) — nothing waits. True = the round-3 behaviour instead: the mix-derived c' = (x - x')/L,
+    # which needs same-round snapshots, so the mix waits for every live neighbour's round-r post.
+    drift_same_round_mix: bool = False
+    drift_exchange: str = "auto"        # auto | on | off: exchanged control variates (auto = on for
+                                        # multi-rank async mailbox gossip, where mixes are stale;
+                                        # identical to the mix-derived form under exact mixing)
+    drift_stale_compensation: str = "none"  # exchange mode, stale mixes: advance a k-round-old
+                                            # neighbour view to the present in the mix — "own":
+                                            # + k * (this client's own update of the round),
+                                            # "global": - k * L * c_hat (fl/drift.py)
+    gossip_stale_decay: float = 0.0     # async mailbox mix: a view k rounds behind keeps
+                                        # W / (1 + decay * k) of its weight (rest -> self)
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
                                         # (matched send/recv); auto = mailbox when async, else rccl
     verify_updates: bool = True         # receivers re-hash every received payload vs its root
@@ -153,6 +164,8 @@ class FLConfig:
                    "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
                    "server_transport": ("rccl", "mailbox"),
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
+                   "drift_exchange": ("auto", "on", "off"),
+                   "drift_stale_compensation": ("none", "own", "global"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
                    "fedavg_weighting": ("examples", "batches", "uniform"),

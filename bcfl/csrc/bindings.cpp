@@ -463,7 +463,8 @@ void adamw(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> para
 void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
               std::vector<Tensor> grads, std::vector<int64_t> offs, double lr, double b1, double b2,
               double eps, double wd, int64_t step, int64_t mode, double grad_scale,
-              optional<Tensor> corr, double corr_lr, std::vector<Tensor> grads2) {
+              optional<Tensor> corr, double corr_lr, std::vector<Tensor> grads2,
+              optional<Tensor> gscale) {
   check_cuda(master, "master");
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
               v.scalar_type() == at::kFloat, "AdamW state must be fp32");
@@ -492,6 +493,10 @@ void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
   }
   const bool po = param_out.has_value() && param_out->defined();
   const bool hc = corr.has_value() && corr->defined();
+  const bool hg = gscale.has_value() && gscale->defined();
+  if (hg)
+    TORCH_CHECK(gscale->is_cuda() && gscale->scalar_type() == at::kFloat && gscale->numel() >= 1,
+                "gscale must be a device fp32 tensor");
   if (hc)
     TORCH_CHECK(corr->is_cuda() && corr->scalar_type() == at::kFloat && corr->is_contiguous() &&
                 corr->numel() == master.numel(), "drift correction must be a flat fp32 buffer");
@@ -501,8 +506,44 @@ void adamw_mt(Tensor master, Tensor m, Tensor v, optional<Tensor> param_out,
                                  numels.data(), (int)ptrs.size(), gdt, (float)lr, (float)b1,
                                  (float)b2, (float)eps, (float)wd, (int)step, (int)mode,
                                  (float)grad_scale, hc ? corr->data_ptr<float>() : nullptr,
-                                 (float)corr_lr, stream(), ptrs2.empty() ? nullptr : ptrs2.data()),
+                                 (float)corr_lr, stream(), ptrs2.empty() ? nullptr : ptrs2.data(),
+                                 hg ? gscale->data_ptr<float>() : nullptr),
            "adamw_mt");
+}
+
+// [clip coefficient, global norm] of a multi-tensor gradient set (grads2: optional second
+// gradient per tensor, summed), as a 2-element device tensor: no host sync between the norm and
+// the AdamW step that consumes the coefficient
+Tensor grad_clip_coef(std::vector<Tensor> grads, std::vector<Tensor> grads2, double max_norm) {
+  TORCH_CHECK(!grads.empty(), "no gradients");
+  TORCH_CHECK(grads2.empty() || grads2.size() == grads.size(), "grads2 must match grads");
+  const int gdt = dt_of(grads[0]);
+  std::vector<Tensor> keep;
+  std::vector<const void*> ptrs, ptrs2;
+  std::vector<int64_t> numels;
+  for (size_t i = 0; i < grads.size(); ++i) {
+    Tensor g = grads[i].is_contiguous() ? grads[i] : grads[i].contiguous();
+    TORCH_CHECK(g.is_cuda() && dt_of(g) == gdt, "gradients must share one dtype on the GPU");
+    keep.push_back(g);
+    ptrs.push_back(g.data_ptr());
+    numels.push_back(g.numel());
+    if (!grads2.empty()) {
+      Tensor h = grads2[i].is_contiguous() ? grads2[i] : grads2[i].contiguous();
+      TORCH_CHECK(h.is_cuda() && dt_of(h) == gdt && h.numel() == g.numel(), "grads2 shape / dtype");
+      keep.push_back(h);
+      ptrs2.push_back(h.data_ptr());
+    }
+  }
+  const int64_t nb = bcfl::sumsq_mt_blocks(numels.data(), (int)numels.size());
+  auto opts = grads[0].options().dtype(at::kFloat);
+  Tensor partial = torch::empty({nb > 0 ? nb : 1}, opts);
+  Tensor out = torch::empty({2}, opts);
+  check_rc(bcfl::launch_clip_coef_mt(ptrs.data(), ptrs2.empty() ? nullptr : ptrs2.data(),
+                                     numels.data(), (int)numels.size(), gdt,
+                                     partial.data_ptr<float>(), (float)max_norm,
+                                     out.data_ptr<float>(), stream()),
+           "grad_clip_coef");
+  return out;
 }
 
 void mix(Tensor master, std::vector<Tensor> nbrs, double self_w, std::vector<double> w,
@@ -900,6 +941,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("adamw", &adamw);
   m.def("adamw_mt", &adamw_mt);
+  m.def("grad_clip_coef", &grad_clip_coef);
   m.def("mix", &mix);
   m.def("axpby", &axpby);
   m.def("cast_copy", &cast_copy);

@@ -301,9 +301,13 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
     float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
     bf16_t* __restrict__ pout_bf, float* __restrict__ pout_f, MTArgs a, int64_t chunk, float b1,
     float b2, float eps, float step_size, float decay_mul, float denom_scale, int hf,
-    float grad_scale, const float* __restrict__ corr, float corr_lr) {
+    float grad_scale, const float* __restrict__ corr, float corr_lr,
+    const float* __restrict__ gscale) {
   // corr (optional): drift-correction direction in update space (SCAFFOLD-style control variate
   // difference c - c_i, bcfl/fl/drift.py); the step becomes p -= lr * (adam_update + corr)
+  // gscale (optional, device): global-norm clip coefficient from clip_coef_kernel, multiplied
+  // into grad_scale (no host round trip between the norm and the step)
+  if (gscale) grad_scale *= gscale[0];
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   int64_t hi = lo + chunk;
   if (hi > a.start[a.n]) hi = a.start[a.n];
@@ -357,6 +361,74 @@ __global__ __launch_bounds__(EW_THREADS) void adamw_mt_kernel(
         if (pout_f) pout_f[f + k] = p;
       }
     }
+  }
+}
+
+// Global gradient norm for clipping: per-block partial sums of squares over the same
+// multi-tensor table as adamw_mt_kernel (g + g2 when a micro-batch replica is attached), then ONE
+// block reduces the partials in a fixed order (deterministic) into [coef, norm] with
+// coef = min(1, max_norm / (norm + 1e-6)) — torch.nn.utils.clip_grad_norm_ semantics.
+template <typename TG>
+__global__ __launch_bounds__(EW_THREADS) void sumsq_mt_kernel(MTArgs a, int64_t chunk,
+                                                               float* __restrict__ partial) {
+  __shared__ float red[EW_THREADS / WAVE];
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  int64_t hi = lo + chunk;
+  if (hi > a.start[a.n]) hi = a.start[a.n];
+  int t = 0;
+  while (t + 1 < a.n && a.start[t + 1] <= lo) ++t;
+  float acc = 0.f;
+  for (int64_t e = lo + threadIdx.x * 4; e < hi; e += EW_THREADS * 4) {
+    while (e >= a.start[t + 1]) ++t;
+    const int64_t loc = e - a.start[t];
+    const int64_t n = a.numel[t];
+    if (loc >= n) continue;
+    const TG* g = reinterpret_cast<const TG*>(a.g[t]) + loc;
+    if (loc + 4 <= n && a.aligned[t]) {
+      float gv[4];
+      Vec4<TG>::load(g, gv);
+      if (a.g2[t]) {
+        float gw[4];
+        Vec4<TG>::load(reinterpret_cast<const TG*>(a.g2[t]) + loc, gw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gv[k] += gw[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += gv[k] * gv[k];
+    } else {
+      for (int k = 0; k < 4 && loc + k < n; ++k) {
+        float gk = ld<TG>(g, k);
+        if (a.g2[t]) gk += ld<TG>(reinterpret_cast<const TG*>(a.g2[t]) + loc, k);
+        acc += gk * gk;
+      }
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+    for (int w = 0; w < EW_THREADS / WAVE; ++w) b += red[w];
+    partial[blockIdx.x] = b;
+  }
+}
+
+__global__ __launch_bounds__(EW_THREADS) void clip_coef_kernel(const float* __restrict__ partial,
+                                                                int n, float max_norm,
+                                                                float* __restrict__ out) {
+  __shared__ float red[EW_THREADS / WAVE];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += EW_THREADS) acc += partial[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < EW_THREADS / WAVE; ++w) s += red[w];
+    const float norm = sqrtf(s);
+    const float c = max_norm / (norm + 1e-6f);
+    out[0] = c < 1.f ? c : 1.f;
+    out[1] = norm;
   }
 }
 
@@ -567,7 +639,7 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
                     const void* const* grads, const int64_t* offs, const int64_t* numels,
                     int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
                     int step, int mode, float grad_scale, const float* corr, float corr_lr,
-                    hipStream_t s, const void* const* grads2) {
+                    hipStream_t s, const void* const* grads2, const float* gscale) {
   const double bc1 = 1.0 - __builtin_pow((double)b1, step);
   const double bc2 = 1.0 - __builtin_pow((double)b2, step);
   const int hf = mode == 0;
@@ -597,12 +669,59 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
     if (grad_dt == DT_BF16)
       hipLaunchKernelGGL(adamw_mt_kernel<bf16_t>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
                          pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
-                         grad_scale, corr, corr_lr);
+                         grad_scale, corr, corr_lr, gscale);
     else
       hipLaunchKernelGGL(adamw_mt_kernel<float>, dim3(grid), dim3(EW_THREADS), 0, s, master, m, v,
                          pb, pf, a, CHUNK, b1, b2, eps, step_size, decay_mul, denom_scale, hf,
-                         grad_scale, corr, corr_lr);
+                         grad_scale, corr, corr_lr, gscale);
   }
+  return 0;
+}
+
+static constexpr int64_t kSumsqChunk = 16384;
+
+int64_t sumsq_mt_blocks(const int64_t* numels, int ntens) {
+  int64_t blocks = 0;
+  for (int g0 = 0; g0 < ntens; g0 += MT_MAX) {
+    const int n = ntens - g0 < MT_MAX ? ntens - g0 : MT_MAX;
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) total += (numels[g0 + i] + 3) / 4 * 4;
+    blocks += (total + kSumsqChunk - 1) / kSumsqChunk;
+  }
+  return blocks;
+}
+
+int launch_clip_coef_mt(const void* const* grads, const void* const* grads2, const int64_t* numels,
+                        int ntens, int grad_dt, float* partial, float max_norm, float* out,
+                        hipStream_t s) {
+  const int esz = grad_dt == DT_BF16 ? 2 : 4;
+  int64_t base = 0;
+  for (int g0 = 0; g0 < ntens; g0 += MT_MAX) {
+    MTArgs a{};
+    a.n = ntens - g0 < MT_MAX ? ntens - g0 : MT_MAX;
+    a.start[0] = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.g[i] = grads[g0 + i];
+      a.g2[i] = grads2 ? grads2[g0 + i] : nullptr;
+      a.off[i] = 0;
+      a.numel[i] = numels[g0 + i];
+      a.start[i + 1] = a.start[i] + (numels[g0 + i] + 3) / 4 * 4;
+      a.aligned[i] = (((uintptr_t)grads[g0 + i]) % (4 * esz) == 0) &&
+                     (((uintptr_t)a.g2[i]) % (4 * esz) == 0);
+    }
+    const int64_t total = a.start[a.n];
+    const unsigned grid = (unsigned)((total + kSumsqChunk - 1) / kSumsqChunk);
+    if (grid == 0) continue;
+    if (grad_dt == DT_BF16)
+      hipLaunchKernelGGL(sumsq_mt_kernel<bf16_t>, dim3(grid), dim3(EW_THREADS), 0, s, a,
+                         kSumsqChunk, partial + base);
+    else
+      hipLaunchKernelGGL(sumsq_mt_kernel<float>, dim3(grid), dim3(EW_THREADS), 0, s, a,
+                         kSumsqChunk, partial + base);
+    base += grid;
+  }
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(EW_THREADS), 0, s, partial, (int)base,
+                     max_norm, out);
   return 0;
 }
 

@@ -73,7 +73,12 @@ int launch_adamw_mt(float* master, float* m, float* v, void* param_out, int para
                     const void* const* grads, const int64_t* offs, const int64_t* numels,
                     int ntens, int grad_dt, float lr, float b1, float b2, float eps, float wd,
                     int step, int mode, float grad_scale, const float* corr, float corr_lr,
-                    hipStream_t s, const void* const* grads2 = nullptr);
+                    hipStream_t s, const void* const* grads2 = nullptr,
+                    const float* gscale = nullptr);
+int64_t sumsq_mt_blocks(const int64_t* numels, int ntens);
+int launch_clip_coef_mt(const void* const* grads, const void* const* grads2, const int64_t* numels,
+                        int ntens, int grad_dt, float* partial, float max_norm, float* out,
+                        hipStream_t s);
 int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
                         float* out, hipStream_t s);
 

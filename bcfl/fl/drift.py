@@ -26,10 +26,30 @@ MI355X-first formulation — no extra communication and one fused term in the op
 Measured (CPU, tiny-bert, 8 one-class clients, 16 rounds, /tmp-free test in tests/test_fl.py):
 without correction the global accuracy peaks near 0.95 and collapses back to 0.5; with it both
 server FedAvg and serverless gossip reach >= 0.99 and stay there.
+
+**Asynchronous gossip (exchanged control variates).** ``c' = (x - x') / L`` is exact only when
+``x'`` mixes models trained in the SAME round from the same start. An asynchronous multi-rank
+federation mixes whatever neighbour snapshot is newest (stale by one or more rounds), and a stale
+label-shard model carries its client's old per-class pull, so ``(x - x') / L`` no longer estimates
+``c`` (2 ranks on one MI355X stayed at the majority rate, profiles/multirank_learning_r3.json).
+With ``exchange=True`` every client instead keeps its own control variate explicitly and
+PUBLISHES it with its model, in the same versioned, Merkle-committed mailbox payload
+(``[model | c_i]``, so a model and its control variate always come from the same version):
+
+* round start (``attach``): ``cv_i <- x_i`` (the start model, needed for ``c_i'``);
+* after training (``after_train``): ``c_i' = (x_i - y_i) / L - s * d_i`` — SCAFFOLD option II,
+  the client's mean update direction with the applied correction removed;
+* after the exchange (``after_exchange``): ``d_i = sum_j W_ij c_j' - c_i'`` over the newest
+  verified snapshots of the neighbours (whatever round they are from) — the stale-exact
+  federation control variate, no waiting on any peer.
+
+Under exact same-round mixing on a complete graph both formulations give the identical
+``d_i' = (y_i - x') / L + s * d_i`` (``tests/test_fl.py::test_drift_exchange_matches_mix_derived``);
+the exchange costs one extra bf16 copy of the parameters on the wire per post.
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, Optional
+from typing import Dict, Iterable, Optional, Sequence
 
 import torch
 
@@ -54,20 +74,46 @@ class DriftCorrection:
             raise ValueError(f"drift_correction must be one of {MODES}, got {mode!r}")
         self.mode, self.scale = mode, float(scale)
         self.enabled = mode != "none"
+        self.clients = list(clients)
+        self.numel, self.device = numel, device
         self.buf: Dict[int, torch.Tensor] = {}
         self.ready: Dict[int, bool] = {}
         self.lr_sum: Dict[int, float] = {}
+        self.exchange = False
+        self.stale_compensation = "none"
+        self._pending: Dict[int, Optional[tuple]] = {}
+        self.cv: Dict[int, torch.Tensor] = {}   # exchange mode: own control variate c_i
         if self.enabled:
-            for c in clients:
+            for c in self.clients:
                 self.buf[c] = torch.zeros(numel, dtype=torch.float32, device=device)
                 self.ready[c] = False
 
-    def attach(self, opt, c: int) -> None:
-        """Before client ``c``'s local steps: its optimizer applies ``d_c`` (round 0: nothing)."""
+    def use_exchange(self) -> Dict[int, torch.Tensor]:
+        """Switch to exchanged control variates (asynchronous gossip); returns the per-client
+        ``c_i`` buffers the gossip engine publishes beside the models."""
+        if not self.enabled:
+            raise RuntimeError("use_exchange() without drift correction")
+        self.exchange = True
+        for c in self.clients:
+            if c not in self.cv:
+                self.cv[c] = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        return self.cv
+
+    def drop_exchange(self) -> None:
+        self.exchange = False
+        self.cv = {}
+
+    def attach(self, opt, c: int, start: Optional[torch.Tensor] = None) -> None:
+        """Before client ``c``'s local steps: its optimizer applies ``d_c`` (round 0: nothing).
+        Exchange mode: ``start`` (the round-start model) is kept for ``c_c'``."""
         if not self.enabled:
             return
         opt.corr = self.buf[c] if self.ready[c] else None
         opt.corr_scale = self.scale
+        if self.exchange:
+            if start is None:
+                raise ValueError("exchanged control variates need the round-start model")
+            self.cv[c].copy_(start)
 
     @staticmethod
     def detach(opt) -> None:
@@ -75,26 +121,86 @@ class DriftCorrection:
 
     @torch.no_grad()
     def after_train(self, c: int, trained: torch.Tensor, lr_sum: float) -> None:
-        """``buf <- y_c / L + s * d_c`` (stream-ordered after the client's last optimizer step)."""
+        """Mix-derived: ``buf <- y_c / L + s * d_c``. Exchange: ``cv <- (x_c - y_c) / L - s * d_c``
+        (stream-ordered after the client's last optimizer step)."""
         if not self.enabled or lr_sum <= 0:
             return
         self.lr_sum[c] = float(lr_sum)
+        if self.exchange:
+            ops.axpby_(self.cv[c], trained, -1.0 / lr_sum, 1.0 / lr_sum)
+            if self.ready[c]:
+                ops.axpby_(self.cv[c], self.buf[c], -self.scale, 1.0)
+            return
         ops.axpby_(self.buf[c], trained, 1.0 / lr_sum, self.scale if self.ready[c] else 0.0)
 
     @torch.no_grad()
     def after_mix(self, c: int, aggregated: torch.Tensor) -> None:
-        """``d_c' = buf - x'_c / L`` once the client's post-aggregation model is known."""
-        if not self.enabled or c not in self.lr_sum:
+        """``d_c' = buf - x'_c / L`` once the client's post-aggregation model is known
+        (mix-derived mode; exchange mode forms ``d_c`` in :meth:`after_exchange`)."""
+        if not self.enabled or self.exchange or c not in self.lr_sum:
             return
         ops.axpby_(self.buf[c], aggregated, -1.0 / self.lr_sum.pop(c), 1.0)
         self.ready[c] = True
+
+    @torch.no_grad()
+    def begin(self, c: int, self_w: float, views: Sequence[torch.Tensor],
+              weights: Sequence[float], age: float = 0.0):
+        """Exchange mode, BEFORE the model mix: remembers the neighbours' published control
+        variates ``views`` (any dtype) and live weights for :meth:`end`. With staleness
+        compensation and a stale mix (``age`` = weighted rounds the neighbours' snapshots are
+        behind) returns extra model-mix terms that advance the stale views to the present:
+
+        * ``"own"``: + age * (y_c - x_c) = -age * L * (c_c' + s * d_c) — this client's own update
+          of the round stands in for what each neighbour did since its snapshot;
+        * ``"global"``: -age * L * c_hat (needs c_hat first, so it is formed here)."""
+        if not (self.enabled and self.exchange) or c not in self.lr_sum:
+            return None
+        L = self.lr_sum.pop(c)
+        self._pending[c] = (float(self_w), list(views), [float(w) for w in weights])
+        mode = self.stale_compensation
+        if not mode or mode == "none" or age <= 0 or not self.ready[c]:
+            return None
+        if mode == "own":
+            return [(self.cv[c], -L * float(age)), (self.buf[c], -L * float(age) * self.scale)]
+        if mode == "global":
+            d = self.buf[c]
+            d.copy_(self.cv[c])
+            ops.gossip_mix_(d, list(views), float(self_w), [float(w) for w in weights])
+            self._pending[c] = None          # buf already holds c_hat
+            return [(d, -L * float(age))]
+        raise ValueError(f"unknown drift_stale_compensation {mode!r}")
+
+    @torch.no_grad()
+    def end(self, c: int) -> None:
+        """After the model mix: ``d_c = c_hat - c_c'`` with
+        ``c_hat = self_w * c_c' + sum_j w_j c_j'`` (fp32 accumulate in the mix kernel)."""
+        if c not in self._pending:
+            return
+        p = self._pending.pop(c)
+        d = self.buf[c]
+        if p is not None:
+            self_w, views, weights = p
+            d.copy_(self.cv[c])
+            ops.gossip_mix_(d, views, self_w - 1.0, weights)
+        else:
+            ops.axpby_(d, self.cv[c], -1.0, 1.0)
+        self.ready[c] = True
+
+    def after_exchange(self, c: int, self_w: float, views: Sequence[torch.Tensor],
+                       weights: Sequence[float]) -> None:
+        """:meth:`begin` + :meth:`end` without a model mix in between."""
+        self.begin(c, self_w, views, weights)
+        self.end(c)
 
     # ---- resume -------------------------------------------------------------------------
     def state_dict(self) -> Optional[dict]:
         if not self.enabled:
             return None
-        return {"buf": {int(c): t.detach().cpu().clone() for c, t in self.buf.items()},
-                "ready": {int(c): bool(v) for c, v in self.ready.items()}}
+        st = {"buf": {int(c): t.detach().cpu().clone() for c, t in self.buf.items()},
+              "ready": {int(c): bool(v) for c, v in self.ready.items()}}
+        if self.exchange:
+            st["cv"] = {int(c): t.detach().cpu().clone() for c, t in self.cv.items()}
+        return st
 
     @torch.no_grad()
     def load_state_dict(self, st: Optional[dict]) -> None:
@@ -104,3 +210,6 @@ class DriftCorrection:
             self.buf[int(c)].copy_(t)
         for c, v in st["ready"].items():
             self.ready[int(c)] = bool(v)
+        if self.exchange and "cv" in st:
+            for c, t in st["cv"].items():
+                self.cv[int(c)].copy_(t)

@@ -134,7 +134,7 @@ class Federation:
             D.broadcast_(self.flat.master, 0)
             self.flat.sync_param_from_master()
         self.opt = FlatAdamW(self.flat, cfg.lr, cfg.adam_betas, cfg.adam_eps, cfg.weight_decay,
-                             cfg.adam_mode)
+                             cfg.adam_mode, cfg.max_grad_norm)
         self.trainer = LocalTrainer(self.model, self.flat, self.opt)
         # ---------------- clients ---------------------------------------------------------------
         n = cfg.num_clients
@@ -179,7 +179,9 @@ class Federation:
         # ---------------- gossip -------------------------------------------------------------------
         if cfg.gossip_transport not in ("auto", "mailbox", "rccl"):
             raise ValueError(f"unknown gossip_transport {cfg.gossip_transport!r}")
-        # drift correction across ranks: mix same-round snapshots (FLConfig.drift_same_round_mix)
+        # drift correction across ranks: async mailbox gossip exchanges the clients' control
+        # variates with their models (stale-exact SCAFFOLD, fl/drift.py) and never waits;
+        # FLConfig.drift_same_round_mix instead waits for every neighbour's round-r snapshot
         self.same_round_mix = bool(cfg.mode == "serverless" and cfg.async_gossip
                                    and cfg.drift_same_round_mix and self.drift.enabled
                                    and self.rt.distributed)
@@ -187,6 +189,11 @@ class Federation:
         if self.transport == "auto":
             # deterministic: the lock-step engine mixes exactly the previous round's states
             self.transport = "mailbox" if (cfg.async_gossip and not cfg.deterministic) else "rccl"
+        cv_exchange = (cfg.mode == "serverless" and not cfg.compat_chain and self.drift.enabled
+                       and self.transport == "mailbox"
+                       and (cfg.drift_exchange == "on" or (
+                           cfg.drift_exchange == "auto" and self.rt.distributed
+                           and cfg.async_gossip and not self.same_round_mix)))
         # A mailbox federation never waits on a peer: the per-round path is collective-free
         # (metrics, evaluation and ledger are rank-local) so a slow or exited rank cannot stall
         # the others. The update anomaly filter needs a global view and keeps its collectives.
@@ -210,6 +217,7 @@ class Federation:
             states = ({c: self.client_master[c] for c in self.local_clients} if self.multi
                       else {self.local_clients[0]: self.flat.master})
             if self.transport == "mailbox":
+                aux = self.drift.use_exchange() if cv_exchange else None
                 try:
                     self.gossip = MailboxGossip(n, states, self.nbrs,
                                                 "fp32" if cfg.wire_dtype == "fp32" else "bf16",
@@ -219,7 +227,10 @@ class Federation:
                                                 # (its later posts bring it back), not waited on
                                                 sync_timeout_s=10.0 if self.same_round_mix else 60.0,
                                                 liveness_timeout=cfg.liveness_timeout,
-                                                verify=cfg.verify_updates)
+                                                verify=cfg.verify_updates, aux=aux,
+                                                aux_sink=self.drift if aux else None)
+                    self.drift.stale_compensation = cfg.drift_stale_compensation
+                    self.gossip.stale_decay = float(cfg.gossip_stale_decay)
                 except MailboxUnavailable as e:
                     # every rank sees the same outcome (agreed collectively in the transport):
                     # fall back together to the lock-step RCCL engine
@@ -227,12 +238,16 @@ class Federation:
                                   "RCCL send/recv (lock-step)", RuntimeWarning)
                     self.transport = "rccl"
                     self.collective_free = False
+                    self.drift.drop_exchange()
             if self.transport != "mailbox":
                 wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
                 if cfg.wire_dtype == "bf16_raw":
                     wire = "bf16"
-                self.gossip = GossipEngine(n, states, self.nbrs, wire,
-                                           cfg.async_gossip and not self.same_round_mix,
+                # the lock-step engine mixes stale-by-one states when async; drift correction
+                # across ranks needs exactly mixed rounds there (the mix-derived c' = (x - x')/L)
+                rccl_async = cfg.async_gossip and not (self.drift.enabled and self.rt.distributed)
+                self.same_round_mix = bool(cfg.async_gossip and not rccl_async)
+                self.gossip = GossipEngine(n, states, self.nbrs, wire, rccl_async,
                                            liveness_timeout=cfg.liveness_timeout,
                                            verify=cfg.verify_updates)
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
@@ -311,7 +326,7 @@ class Federation:
                 flat = FlatParams.from_model(model, self.device, mdtype)
                 flat.load_master(self.flat.master)
                 opt = FlatAdamW(flat, cfg.lr, cfg.adam_betas, cfg.adam_eps, cfg.weight_decay,
-                                cfg.adam_mode)
+                                cfg.adam_mode, cfg.max_grad_norm)
                 tr = LocalTrainer(model, flat, opt)
             stream = torch.cuda.Stream(device=self.device) if self.is_cuda else None
             lanes.append(ClientLane(i, model, flat, opt, tr, stream,
@@ -368,7 +383,7 @@ class Federation:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
-                self.drift.attach(lane.opt, c)
+                self.drift.attach(lane.opt, c, lane.flat.master)
                 prev = lane.flat.master.detach().clone() if need_prev else None
                 loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
             st = {"batches": 0, "tokens": 0, "examples": 0}
@@ -445,7 +460,7 @@ class Federation:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
-                self.drift.attach(lane.opt, c)
+                self.drift.attach(lane.opt, c, lane.flat.master)
                 loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
             st = {"batches": 0, "tokens": 0, "examples": 0}
             for e in range(cfg.local_epochs):
@@ -715,7 +730,7 @@ class Federation:
             self.opt.load_state_dict(self.client_opt[c])
         else:
             self.opt.reset()
-        self.drift.attach(self.opt, c)
+        self.drift.attach(self.opt, c, self.flat.master)
         ops.rng.global_rng().load_state(self.client_rng[c])
 
     def _deactivate(self, c: int):
@@ -970,9 +985,19 @@ class Federation:
                 self.acc.copy_(g_new)
                 wire_bytes = minfo["bytes_sent"]
                 absent = minfo["absent_ranks"]
+                # ledger: this rank's post is an update block and every verified receive a verify
+                # block, both keyed by the sending rank's id -(rank + 1) and the post's version,
+                # so audit_ledgers() matches every accepted receive against its commitment
                 for g in self.server_mbox.take_records():
-                    if g["kind"] == "recv":
-                        recs.append({"client": -1, "kind": "verify", "root": g["root"],
+                    if g["kind"] == "update":
+                        rt_ = g.get("root_t")
+                        recs.append({"client": g["client"], "kind": "update",
+                                     "root": "" if rt_ is None else ops.root_bytes(rt_).hex(),
+                                     "verdict": "accept", "ts": float(r) + 0.4,
+                                     "metrics": {"sender_rank": self.rt.rank,
+                                                 "version": g["version"]}})
+                    elif g["kind"] == "recv":
+                        recs.append({"client": g["client"], "kind": "verify", "root": g["root"],
                                      "verdict": "accept" if g["ok"] else "reject",
                                      "ts": float(r) + 0.5,
                                      "metrics": {"sender_rank": -g["client"] - 1,
@@ -1015,14 +1040,23 @@ class Federation:
         extra = {"kind": "global", "root": self._merkle() if self.ledger else "",
                  "rejected": sorted(v.rejected)}
         if self.server_mbox is not None:
-            extra.update(absent_ranks=absent, live_weight=self._server_live["live_weight"])
+            extra.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
+                         rejoined_ranks=self._server_live["rejoined_ranks"],
+                         view_mismatch=self._server_live["view_mismatch"])
+            if self._server_live["view_mismatch"]:
+                warnings.warn(f"round {r}: rank(s) {self._server_live['view_mismatch']} aggregated "
+                              "a different live-rank set last round than this rank (a timed-out "
+                              "but live peer): the global models differed for that round",
+                              RuntimeWarning)
         self._ledger_round(r, recs, extra)
         out = {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
                "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                "client_metrics": client_metrics, "bytes_sent": float(wire_bytes)}
         if self.server_mbox is not None:
             out.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
-                       dead_peers=sorted(self.server_mbox.dead))
+                       dead_peers=sorted(self.server_mbox.dead),
+                       view_mismatch=self._server_live["view_mismatch"],
+                       rejoined_ranks=self._server_live["rejoined_ranks"])
         return out
 
     @property
@@ -1150,6 +1184,7 @@ class Federation:
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                 "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
                 "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
+                "stale_max": info.get("stale_max", 0.0), "wait_s": info.get("wait_s", 0.0),
                 "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
                 "rejected_msgs": info.get("rejected_msgs", 0.0)}
 
@@ -1213,8 +1248,9 @@ class Federation:
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
                "dead_peers": res.get("dead_peers", []),
-               **{k: res[k] for k in ("mixed", "stale_rounds", "torn", "rejected_msgs",
-                                      "absent_ranks", "live_weight") if k in res},
+               **{k: res[k] for k in ("mixed", "stale_rounds", "stale_max", "wait_s", "torn",
+                                      "rejected_msgs", "absent_ranks", "live_weight",
+                                      "view_mismatch", "rejoined_ranks") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
         if self.is_cuda:
@@ -1235,14 +1271,17 @@ class Federation:
         ``save_clients``, and with ``save_resume_state`` the per-rank state a resumed run needs to
         continue bit-identically (``<out>/resume/rank{r}.pt``)."""
         cfg = self.cfg
-        if self.ckpt is None or (r + 1) % cfg.save_every:
+        if cfg.save_every <= 0 or (r + 1) % cfg.save_every:
             return
         pend = self._eval_pending
         if pend is not None and pend[0] == r and not self.collective_free and self.rt.distributed:
             # multi-rank collective mode: the saved accuracy is the job's (all-reduced), so
-            # resolve here, where every rank is (before the per-rank busy-skip below); one rank
-            # holds the whole job's statistics and leaves this to the writer thread
+            # resolve here — on EVERY rank, including those that write nothing (self.ckpt None):
+            # the resolve is a collective, and a rank skipping it would pair its next all-reduce
+            # with the others' FedAvg all-reduce
             self._resolve_eval()
+        if self.ckpt is None:
+            return
         if self.ckpt.busy():
             if cfg.save_resume_state:
                 # resumable runs never skip: every rank's files of a save belong to ONE round
@@ -1306,11 +1345,21 @@ class Federation:
             st["gossip"] = self.gossip.state_dict()
         return st
 
+    def next_round(self, r: int) -> int:
+        """Round to run after round r: r + 1, except when the mailbox FedAvg joined a later
+        aggregation epoch (this rank started late or was excluded as slow, fedavg.py): the rank
+        then continues at the federation's round instead of replaying the ones it missed."""
+        if self.server_mbox is not None:
+            return max(r + 1, self.server_mbox.epoch)
+        return r + 1
+
     def run(self, rounds: Optional[int] = None) -> List[dict]:
         cfg = self.cfg
         end = cfg.num_rounds if rounds is None else self.start_round + rounds
-        for r in range(self.start_round, end):
+        r = self.start_round
+        while r < end:
             self.run_round(r)
+            r = self.next_round(r)
         self.finish()
         return self.history
 

@@ -35,14 +35,17 @@ def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], 
                  lr: float, beta1: float, beta2: float, eps: float, weight_decay: float,
                  mode: str = "hf", param_out: Optional[torch.Tensor] = None,
                  grad_scale: float = 1.0, corr: Optional[torch.Tensor] = None,
-                 corr_lr: float = 0.0, grads2: Optional[Sequence[torch.Tensor]] = None):
+                 corr_lr: float = 0.0, grads2: Optional[Sequence[torch.Tensor]] = None,
+                 gscale: Optional[torch.Tensor] = None):
     """AdamW where each gradient is its own tensor (as autograd produced it) and master / m / v /
     param live in flat buffers at ``offsets``: one multi-tensor launch per <=40 tensors.
 
     ``corr`` (flat fp32, optional): drift correction in update space, applied in the same pass as
     ``p -= corr_lr * corr`` on every element that received a gradient (bcfl.fl.drift).
     ``grads2`` (optional, aligned with ``grads``): a second gradient of each tensor — the
-    micro-batch replica's — summed in the same pass (no separate accumulation kernel)."""
+    micro-batch replica's — summed in the same pass (no separate accumulation kernel).
+    ``gscale`` (optional, device fp32 ``[coef, ...]``): a gradient multiplier read on the device
+    (the global-norm clip coefficient of :func:`grad_clip_coef`)."""
     if not grads:
         return
     if grads2 is not None and len(grads2) != len(grads):
@@ -51,10 +54,12 @@ def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], 
         native().adamw_mt(master, m, v, param_out, list(grads), [int(o) for o in offsets],
                           float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
                           int(step), 0 if mode == "hf" else 1, float(grad_scale), corr,
-                          float(corr_lr), list(grads2) if grads2 is not None else [])
+                          float(corr_lr), list(grads2) if grads2 is not None else [], gscale)
         return
     if grads2 is not None:
         grads = [g + g2 for g, g2 in zip(grads, grads2)]
+    if gscale is not None:
+        grad_scale = grad_scale * float(gscale[0])
     for g, o in zip(grads, offsets):
         n = g.numel()
         po = None if param_out is None or param_out.data_ptr() == master.data_ptr() else param_out[o:o + n]
@@ -64,6 +69,26 @@ def adamw_multi_(master, grads: Sequence[torch.Tensor], offsets: Sequence[int], 
             master[o:o + n].sub_(corr[o:o + n], alpha=corr_lr)
             if po is not None:
                 po.copy_(master[o:o + n])
+
+
+def grad_clip_coef(grads: Sequence[torch.Tensor], max_norm: float,
+                   grads2: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+    """``[min(1, max_norm / (||g||_2 + 1e-6)), ||g||_2]`` over all gradients (``g + g2`` per
+    tensor with a micro-batch replica) as a 2-element fp32 tensor on the gradients' device —
+    ``torch.nn.utils.clip_grad_norm_`` semantics, consumed by :func:`adamw_multi_` (``gscale``)
+    without a host sync. GPU: a multi-tensor partial-sum kernel + one deterministic finisher."""
+    if grads2 is not None and len(grads2) != len(grads):
+        raise ValueError("grads2 must align with grads")
+    if grads and use_native(grads[0], "adamw"):
+        return native().grad_clip_coef(list(grads), list(grads2) if grads2 is not None else [],
+                                       float(max_norm))
+    tot = torch.zeros((), dtype=torch.float64, device=grads[0].device if grads else "cpu")
+    for i, g in enumerate(grads):
+        x = g.float() if grads2 is None else g.float() + grads2[i].float()
+        tot += (x.double() ** 2).sum()
+    norm = tot.sqrt().float()
+    coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    return torch.stack([coef, norm])
 
 
 def gossip_mix_(master: torch.Tensor, neighbours: Sequence[torch.Tensor], self_w: float,

@@ -16,8 +16,23 @@ Here every rank is its own aggregator:
    live, verifies each payload's root, and declares the ranks that did not post (or posted a
    payload that fails verification) absent;
 3. the new global model is ``G = sum_{r live} S_r / sum_{r live} W_r`` summed in rank order, so
-   every survivor that saw the same live set computes the bit-identical G; absentees stay out
-   (dead) for the rest of the run and are recorded in each rank's ledger block.
+   every survivor that saw the same live set computes the bit-identical G.
+
+Live-set agreement. Each rank decides on its own which peers missed the timeout, so two ranks can
+disagree (A times out on a slow-but-alive B while B still receives A's post): that round A and B
+compute different G. Two rules keep such a split from becoming permanent:
+
+* every post carries the live-rank set its sender aggregated in the previous round (a bitmask in
+  the header's aux word); a receiver compares it with its own and reports the ranks whose view
+  differed (``view_mismatch``, recorded in the ledger's round block) — a split is never silent;
+* a post's version is the aggregation EPOCH, not the local round: a rank that finds a peer's
+  newest post ahead of its own next epoch (it started late, or was excluded as slow) posts into
+  that epoch, joining the federation's current aggregate (its skipped epochs are reported);
+* an absent rank is not waited on again, but it is not excluded for good either: its inbox is
+  checked (without waiting) every round; if that round's post is there it rejoins at once, and if
+  a NEWER post than the last one seen is there (alive but lagging) it is waited on again (bounded)
+  from the next round, which lets it catch up. G only depends on the posted partial sums, so the
+  first round all ranks see the same live set they compute the bit-identical G again.
 
 With every rank live, G equals the all-reduce result (up to the fp32 summation order). Payloads
 are fp32 (exact partial sums); inboxes cost 2 slots x model bytes per peer (7 x 0.87 GB for
@@ -64,19 +79,38 @@ class MailboxFedAvg:
         self.dead: set = set()
         self.records: List[dict] = []
         self.bytes_posted = 0
+        self.prev_live_mask = (1 << self.world) - 1   # the live set of the previous round
+        self.last_seen: Dict[int, int] = {p: 0 for p in self.peers}   # newest version seen
+        self.epoch = 0                                # version of this rank's last post
+        self._sum_done = None                         # event: last reader of the stage buffers
+
+    @staticmethod
+    def _mask(ranks) -> int:
+        m = 0
+        for q in ranks:
+            m |= 1 << int(q)
+        return m
 
     def reduce(self, r: int, partial: torch.Tensor, w_local: float) -> Tuple[torch.Tensor, Dict]:
         """Round r: post ``partial`` (this rank's weighted sum, fp32 flat) with weight
         ``w_local``; return (G, info) with G the re-normalised sum over the live ranks."""
-        v = r + 1
-        slot = v % 2
         tr = self.transport
+        # aggregation epoch = the post's version: one past this rank's last, or — when a peer is
+        # already further (this rank started late or was excluded as slow) — the peer's newest,
+        # so a lagging rank joins the federation's current aggregate instead of waiting for
+        # posts that were overwritten long ago
+        ahead = [nw[1].version for nw in (tr.newest(h) for h in tr.headers(self.peers).values())
+                 if nw is not None]
+        v = max([self.epoch + 1] + ahead)
+        skipped = v - self.epoch - 1
+        self.epoch = v
+        slot = v % 2
         if tr.is_cuda:
             tr.wait_slot_free(self.rank, slot)
         buf = self.send_buf[slot]
         buf.copy_(partial)
         root = ops.merkle_root_deferred(buf) if self.verify else None
-        snap = Snapshot(v, r, _f2i(w_local), buf.numel() * 4, b"\0" * 32)
+        snap = Snapshot(v, r, _f2i(w_local), buf.numel() * 4, b"\0" * 32, self.prev_live_mask)
         rd = root
         if rd is not None and not torch.is_tensor(rd):
             snap.root, rd = bytes(rd), None
@@ -84,19 +118,35 @@ class MailboxFedAvg:
         tr.post(self.rank, buf, snap, rd)
         self.records.append({"client": -(self.rank + 1), "kind": "update", "version": v,
                              "root_t": root})
-        # ---- wait for round r from every rank still counted live ----------------------------
+        # ---- wait (bounded) for round r from every rank counted live; absent ranks are only
+        # checked, never waited on, and rejoin when they post again ---------------------------
         need = [p for p in self.peers if p not in self.dead]
         got: Dict[int, Snapshot] = {}
         t0 = time.perf_counter()
+        after = self._sum_done
         while True:
             left = [p for p in need if p not in got]
             if not left:
                 break
-            got.update(tr.fetch_exact({p: v for p in left}, self.stage))
+            got.update(tr.fetch_exact({p: v for p in left}, self.stage, after=after))
+            after = None
             if all(p in got for p in need) or time.perf_counter() - t0 > self.timeout_s:
                 break
             time.sleep(0.0005)
-        absent = sorted(p for p in need if p not in got)
+        wait_s = time.perf_counter() - t0
+        back = [p for p in self.peers if p in self.dead]
+        lagging = []
+        if back:
+            got.update(tr.fetch_exact({p: v for p in back}, self.stage, after=after))
+            hdr = tr.headers([p for p in back if p not in got])
+            for p, h in hdr.items():
+                nw = tr.newest(h)
+                if nw is not None and nw[1].version > self.last_seen[p]:
+                    lagging.append(p)        # alive: waited on (bounded) again next round
+                    self.last_seen[p] = nw[1].version
+        for p, sn in got.items():
+            self.last_seen[p] = max(self.last_seen[p], sn.version)
+        absent = sorted(p for p in self.peers if p not in got)
         ok = {}
         if got and self.verify:
             fs = tr.fetch_stream
@@ -118,7 +168,11 @@ class MailboxFedAvg:
             if not good:
                 absent.append(p)
         absent = sorted(set(absent))
-        self.dead |= set(absent)
+        rejoined = sorted(p for p in back if p not in absent)
+        self.dead = set(absent) - set(lagging)
+        # ---- live-set agreement: every peer's view of the previous round vs this rank's -------
+        mismatch = sorted(p for p, sn in got.items() if p not in absent and r > 0
+                          and sn.aux != self.prev_live_mask)
         # ---- G = sum_{live} S_r / sum_{live} W_r, in rank order -------------------------------
         live = sorted([self.rank] + [p for p in got if p not in absent])
         out = torch.zeros_like(partial)
@@ -129,8 +183,14 @@ class MailboxFedAvg:
             wsum += w_local if q == self.rank else _i2f(got[q].steps)
         if wsum > 0 and abs(wsum - 1.0) > 1e-12:
             ops.scale_(out, 1.0 / wsum)
+        if tr.is_cuda:  # the next round's fetch may overwrite stage[] only after this sum
+            self._sum_done = torch.cuda.Event()
+            self._sum_done.record(torch.cuda.current_stream(self.device))
+        self.prev_live_mask = self._mask(live)
         self.bytes_posted += tr.bytes_posted - b0
         return out, {"live_ranks": live, "absent_ranks": absent, "live_weight": wsum,
+                     "rejoined_ranks": rejoined, "view_mismatch": mismatch, "wait_s": wait_s,
+                     "epoch": v, "epochs_skipped": skipped,
                      "bytes_sent": float(tr.bytes_posted - b0)}
 
     def take_records(self) -> List[dict]:

@@ -125,9 +125,13 @@ class FlatAdamW:
     optimizer per fit (C8)."""
 
     def __init__(self, flat: FlatParams, lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-6,
-                 weight_decay: float = 0.0, mode: str = "hf"):
+                 weight_decay: float = 0.0, mode: str = "hf", max_grad_norm: float = 0.0):
         self.flat = flat
         self.lr, self.betas, self.eps, self.wd, self.mode = lr, tuple(betas), eps, weight_decay, mode
+        # global-norm gradient clipping (0 = off, the reference's plain loop); the coefficient
+        # stays on the device (ops.grad_clip_coef) and scales the gradients inside the AdamW pass
+        self.max_grad_norm = float(max_grad_norm)
+        self.last_grad_norm: Optional[torch.Tensor] = None
         self.m = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.v = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
         self.step_count = 0
@@ -160,11 +164,16 @@ class FlatAdamW:
                 grads.append(g1 if g1 is not None else torch.zeros_like(g2))
                 grads2.append(g2 if g2 is not None else torch.zeros_like(g1))
                 offs.append(o)
+        gscale = None
+        if self.max_grad_norm > 0 and grads:
+            # clip the TRUE gradient: grad_scale (loss-scale undo) applies before the norm
+            gscale = ops.grad_clip_coef(grads, self.max_grad_norm / grad_scale, grads2)
+            self.last_grad_norm = gscale[1:2] * grad_scale
         ops.adamw_multi_(f.master, grads, offs, self.m, self.v, self.step_count, self.lr,
                          self.betas[0], self.betas[1], self.eps, self.wd, self.mode,
                          param_out=None if f.master is f.param else f.param,
                          grad_scale=grad_scale, corr=self.corr,
-                         corr_lr=self.lr * self.corr_scale, grads2=grads2)
+                         corr_lr=self.lr * self.corr_scale, grads2=grads2, gscale=gscale)
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}

@@ -217,12 +217,17 @@ class GossipEngine:
         return W
 
     @torch.no_grad()
-    def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None):
+    def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None,
+            extra: Optional[Dict[int, tuple]] = None):
+        """``extra[c] = [(tensor, weight), ...]``: more terms of client c's mix (same kernel pass)."""
         for c in self.local:
             nb = [j for j in range(self.n) if j != c and W[c, j] != 0.0]
             views = [self.view(j) for j in nb]
-            ops.gossip_mix_(self.states[c], views, float(W[c, c]), [float(W[c, j]) for j in nb],
-                            (param_out or {}).get(c))
+            ws = [float(W[c, j]) for j in nb]
+            for t, wt in ((extra or {}).get(c) or []):
+                views.append(t)
+                ws.append(float(wt))
+            ops.gossip_mix_(self.states[c], views, float(W[c, c]), ws, (param_out or {}).get(c))
 
     # ------------------------------------------------------------------------------------
     def end_of_round(self, round_idx: int, W: np.ndarray,
@@ -354,12 +359,22 @@ class MailboxGossip:
     ``sync=True`` turns step 2 into a bounded wait: poll until every live neighbour has published
     round r (or ``sync_timeout_s`` passes and it is declared dead) — lock-step semantics without
     any matched transfer, for the sync-vs-async comparison.
+
+    ``aux`` (optional, per hosted client, fp32, same size as the model): a second state published
+    in the SAME payload (``[model | aux]``, one version, one header, one Merkle commitment) — the
+    clients' SCAFFOLD control variates (:mod:`bcfl.fl.drift`, exchange mode). ``aux_sink`` (the
+    drift correction) gets, per hosted client and BEFORE the model mix,
+    ``begin(c, self_w, views, weights, age)`` with the neighbours' aux halves, the live mixing
+    weights and the mix's staleness ``age = sum_j W_cj * (rounds the view of j is behind)``; it
+    may return extra ``[(tensor, weight)]`` terms for client c's model mix (staleness
+    compensation); ``end(c)`` runs after the mix.
     """
 
     def __init__(self, num_clients: int, states: Dict[int, torch.Tensor], nbrs: Dict[int, List[int]],
                  wire: str = "bf16", sync: bool = False, liveness_timeout: int = 2,
                  verify: bool = True, sync_timeout_s: float = 60.0, rank: Optional[int] = None,
-                 world: Optional[int] = None):
+                 world: Optional[int] = None, aux: Optional[Dict[int, torch.Tensor]] = None,
+                 aux_sink=None):
         from .mailbox import MailboxTransport
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
@@ -378,6 +393,11 @@ class MailboxGossip:
         self.verify = verify
         any_state = next(iter(states.values()))
         self.numel, self.device = any_state.numel(), any_state.device
+        self.aux = aux
+        self.aux_sink = aux_sink
+        if aux is not None and sorted(aux) != self.local:
+            raise ValueError("aux states must cover exactly the hosted clients")
+        self.msg_numel = self.numel * (2 if aux is not None else 1)
         self.wire_dtype = torch.float32 if wire == "fp32" else torch.bfloat16
         self.remote_needed = sorted({j for c in self.local for j in nbrs[c]
                                      if client_rank(j, self.world) != self.rank})
@@ -386,9 +406,9 @@ class MailboxGossip:
             dsts = sorted({client_rank(i, self.world) for i in range(self.n) if c in nbrs[i]}
                           - {self.rank})
             send_plan += [(c, r) for r in dsts]
-        self.transport = MailboxTransport(self.numel, self.wire_dtype, self.device,
+        self.transport = MailboxTransport(self.msg_numel, self.wire_dtype, self.device,
                                           self.remote_needed, send_plan, self.rank, self.world)
-        z = lambda: torch.zeros(self.numel, dtype=self.wire_dtype, device=self.device)  # noqa: E731
+        z = lambda: torch.zeros(self.msg_numel, dtype=self.wire_dtype, device=self.device)  # noqa: E731
         self.send_buf = {c: [z(), z()] for c in self.local}
         self.replica = {j: z() for j in self.remote_needed}
         self.stage = {j: z() for j in self.remote_needed}
@@ -404,22 +424,33 @@ class MailboxGossip:
         self.rejected_msgs = 0
         self.records: List[dict] = []  # ledger records of this round (published + verified)
         self._round_local = -1
+        self.wait_s = 0.0              # host time spent waiting for peers (sync mode only)
+        self.stale_decay = 0.0         # see _age_weighted
 
     # ------------------------------------------------------------------------------------
     def seed_replicas(self, initial: torch.Tensor):
         """Every client starts from the identical initial model, so every replica (version 0)
         starts equal to it: a neighbour that never publishes is mixed as the initial model until
-        the staleness bound retires it."""
-        for j in self.remote_needed:
-            ops.cast_copy_(self.replica[j], initial)
-        for c in self.local:
-            ops.cast_copy_(self.send_buf[c][0], initial)
-            ops.cast_copy_(self.send_buf[c][1], initial)
+        the staleness bound retires it. Aux halves (control variates) start at zero."""
+        n = self.numel
+        for t in [self.replica[j] for j in self.remote_needed] + \
+                 [b for c in self.local for b in self.send_buf[c]]:
+            ops.cast_copy_(t[:n], initial)
+            if self.aux is not None:
+                t[n:].zero_()
 
-    def view(self, j: int) -> torch.Tensor:
+    def _msg(self, j: int) -> torch.Tensor:
         if j in self.states:
             return self.send_buf[j][self.version[j] % 2]
         return self.replica[j]
+
+    def view(self, j: int) -> torch.Tensor:
+        """Newest verified model of client j (the model half of its message)."""
+        return self._msg(j)[: self.numel]
+
+    def aux_view(self, j: int) -> torch.Tensor:
+        """Newest verified aux state (control variate) of client j, same version as :meth:`view`."""
+        return self._msg(j)[self.numel:]
 
     @torch.no_grad()
     def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None):
@@ -434,7 +465,9 @@ class MailboxGossip:
             if self.transport.is_cuda:
                 self.transport.wait_slot_free(c, slot)
             buf = self.send_buf[c][slot]
-            ops.cast_copy_(buf, self.states[c])
+            ops.cast_copy_(buf[: self.numel], self.states[c])
+            if self.aux is not None:
+                ops.cast_copy_(buf[self.numel:], self.aux[c])
             roots[c] = ops.merkle_root_deferred(buf) if self.verify else None
             if c in self.tamper:  # in-flight corruption AFTER the commitment was computed
                 buf.view(-1)[: min(64, buf.numel())].add_(1.0)
@@ -475,6 +508,7 @@ class MailboxGossip:
                     self.stage[j], self.scratch[j] = self.scratch[j], self.stage[j]
                 got.update(more)
                 have |= {j for j, s in more.items() if s.round >= round_idx}
+            self.wait_s += _time.perf_counter() - t0
         self.torn = tr.torn
         ok = {}
         if got and self.verify:
@@ -507,26 +541,58 @@ class MailboxGossip:
     def live_matrix(self, W: np.ndarray) -> np.ndarray:
         return GossipEngine.live_matrix(self, W)
 
+    def _age_weighted(self, W: np.ndarray, round_idx: int) -> np.ndarray:
+        """``stale_decay`` > 0: a neighbour view k rounds behind keeps W_cj / (1 + decay * k) of
+        its weight (the rest moves to c's self-weight), so a far-behind snapshot pulls the mix
+        back less; 0 = plain mixing."""
+        if self.stale_decay <= 0:
+            return W
+        W = W.copy()
+        for c in self.local:
+            for j in self.remote_needed:
+                if W[c, j] == 0.0:
+                    continue
+                k = max(0, round_idx - self.replica_round[j])
+                keep = W[c, j] / (1.0 + self.stale_decay * k)
+                W[c, c] += W[c, j] - keep
+                W[c, j] = keep
+        return W
+
     @torch.no_grad()
-    def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None):
-        return GossipEngine.mix(self, W, param_out)
+    def mix(self, W: np.ndarray, param_out: Optional[Dict[int, torch.Tensor]] = None,
+            extra: Optional[Dict[int, tuple]] = None):
+        return GossipEngine.mix(self, W, param_out, extra)
 
     def end_of_round(self, round_idx: int, W: np.ndarray,
                      param_out: Optional[Dict[int, torch.Tensor]] = None,
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
-        b0 = self.transport.bytes_posted
+        b0, w0 = self.transport.bytes_posted, self.wait_s
         self.publish(round_idx, steps)
         self.collect(round_idx)
         self._age_out(round_idx)
         fs = self.transport.fetch_stream
         if fs is not None:  # the mix reads what the fetch stream wrote
             torch.cuda.current_stream(self.device).wait_stream(fs)
-        self.mix(self.live_matrix(W), param_out)
+        Wl = self._age_weighted(self.live_matrix(W), round_idx)
+        extra = {}
+        if self.aux is not None and self.aux_sink is not None:
+            for c in self.local:
+                nb = [j for j in range(self.n) if j != c and Wl[c, j] != 0.0]
+                age = sum(float(Wl[c, j]) * max(0, round_idx - self.replica_round[j])
+                          for j in nb if j not in self.states)
+                extra[c] = self.aux_sink.begin(c, float(Wl[c, c]), [self.aux_view(j) for j in nb],
+                                               [float(Wl[c, j]) for j in nb], age)
+        self.mix(Wl, param_out, extra)
+        if self.aux is not None and self.aux_sink is not None:
+            for c in self.local:
+                self.aux_sink.end(c)
         if fs is not None:  # the next fetch may overwrite the buffers this mix read after this
             self._mix_done = torch.cuda.Event()
             self._mix_done.record(torch.cuda.current_stream(self.device))
         ages = [round_idx - self.replica_round[j] for j in self.remote_needed if j not in self.dead]
         return {"mixed": 1.0, "stale_rounds": float(np.mean(ages)) if ages else 0.0,
+                "stale_max": float(max(ages)) if ages else 0.0,
+                "wait_s": float(self.wait_s - w0),
                 "bytes_sent": float(self.transport.bytes_posted - b0),
                 "dead_peers": float(len(self.dead)), "torn": float(self.torn),
                 "rejected_msgs": float(self.rejected_msgs)}

@@ -37,7 +37,7 @@ import torch
 from . import dist as D
 
 HDR_WORDS = 16
-W_BEGIN, W_ROUND, W_STEPS, W_BYTES, W_ROOT, W_END = 0, 1, 2, 3, 4, 8
+W_BEGIN, W_ROUND, W_STEPS, W_BYTES, W_ROOT, W_END, W_AUX = 0, 1, 2, 3, 4, 8, 9
 ALIGN = 4096
 
 
@@ -61,6 +61,12 @@ class Snapshot:
     steps: int
     nbytes: int
     root: bytes
+    aux: int = 0      # one protocol word (server FedAvg: the sender's previous live-rank set)
+
+
+def _snap(h: np.ndarray, s: int, v: int) -> Snapshot:
+    return Snapshot(v, int(h[s, W_ROUND]), int(h[s, W_STEPS]), int(h[s, W_BYTES]),
+                    words_to_root(h[s, W_ROOT:W_ROOT + 4]), int(h[s, W_AUX]))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -254,6 +260,7 @@ class MailboxTransport:
                     if root_dev is not None:
                         box.hdr[slot, W_ROOT:W_ROOT + 4].copy_(root_dev.view(torch.int64),
                                                                non_blocking=True)
+                    self.backend.hdr_store(box.hdr, slot, [snap.aux], W_AUX)
                     self.backend.hdr_store(box.hdr, slot, body, W_ROUND, W_END, snap.version)
                     ev = torch.cuda.Event()
                     ev.record(st)
@@ -263,6 +270,7 @@ class MailboxTransport:
                 box.slots[slot].copy_(payload)
                 if root_dev is not None:
                     box.hdr[slot, W_ROOT:W_ROOT + 4] = root_dev.view(torch.int64)
+                self.backend.hdr_store(box.hdr, slot, [snap.aux], W_AUX)
                 self.backend.hdr_store(box.hdr, slot, body, W_ROUND, W_END, snap.version)
             self.bytes_posted += self.payload_bytes
         if evs:
@@ -327,8 +335,7 @@ class MailboxTransport:
         for s in (0, 1):
             v = int(h[s, W_BEGIN])
             if v > 0 and v == int(h[s, W_END]) and (best is None or v > best[1].version):
-                best = (s, Snapshot(v, int(h[s, W_ROUND]), int(h[s, W_STEPS]), int(h[s, W_BYTES]),
-                                    words_to_root(h[s, W_ROOT:W_ROOT + 4])))
+                best = (s, _snap(h, s, v))
         return best
 
     def fetch(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
@@ -368,12 +375,16 @@ class MailboxTransport:
             torch.cuda.current_stream(self.device).wait_stream(fs)
         return good
 
-    def fetch_exact(self, want: Dict[int, int], out: Dict[int, torch.Tensor]) -> Dict[int, Snapshot]:
+    def fetch_exact(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
+                    after: Optional["torch.cuda.Event"] = None) -> Dict[int, Snapshot]:
         """Like :meth:`fetch` but for EXACTLY version ``want[j]`` (a slot whose begin == end ==
         that version): round-synchronous protocols (server FedAvg over mailboxes) need round r's
-        post even when the sender has already posted round r + 1 into its other slot."""
+        post even when the sender has already posted round r + 1 into its other slot.
+        ``after``: as in :meth:`fetch` (the ``out`` buffers' last reader)."""
         js = list(want)
         fs = self.fetch_stream
+        if fs is not None and after is not None:
+            fs.wait_event(after)
         first = self.headers(js)
         picked: Dict[int, Tuple[int, Snapshot]] = {}
         for j in js:
@@ -381,9 +392,7 @@ class MailboxTransport:
             for slot in (0, 1):
                 v = int(h[slot, W_BEGIN])
                 if v == want[j] and v == int(h[slot, W_END]):
-                    picked[j] = (slot, Snapshot(v, int(h[slot, W_ROUND]), int(h[slot, W_STEPS]),
-                                                int(h[slot, W_BYTES]),
-                                                words_to_root(h[slot, W_ROOT:W_ROOT + 4])))
+                    picked[j] = (slot, _snap(h, slot, v))
                     if fs is not None:
                         with torch.cuda.stream(fs):
                             out[j].copy_(self.inbox[j].slots[slot], non_blocking=True)

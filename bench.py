@@ -6,7 +6,8 @@ One "step" = one federated ROUND of an 8-client federation: every client trains 
 (240 samples = 8 batches of 32, reference ``serverless_NonIID_IMDB.py:59``), evaluates on its 60
 local test rows, publishes its model into its peers' one-sided hipIpc mailboxes (async: the copies
 to every peer run concurrently on side streams; receivers mix the newest complete snapshot — with
-drift correction across ranks, the round's own snapshot, see FLConfig.drift_same_round_mix),
+drift correction across ranks, each client's SCAFFOLD control variate travels in the same
+post, so the federation control variate is exact for whatever snapshot round is mixed),
 every received payload is re-hashed and checked against its sender's committed Merkle root
 before it is mixed (only at N > 1: with all 8 clients on one rank nothing crosses a process),
 every client model is scored on its stride of a class-balanced 1000-row global draw (overlapped
@@ -76,7 +77,20 @@ def parse():
                     help="override the preset's local batch size (0 = preset)")
     ap.add_argument("--micro-batches", type=int, default=0,
                     help="ranks training one client at a time: 2 = concurrent micro-batches, 1 = off, 0 = auto")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra FLConfig override (JSON value), e.g. --set max_grad_norm=1.0")
     return ap.parse_args()
+
+
+def _overrides(items):
+    out = {}
+    for it in items:
+        k, _, v = it.partition("=")
+        try:
+            out[k.strip()] = json.loads(v)
+        except json.JSONDecodeError:
+            out[k.strip()] = v
+    return out
 
 
 def _launch_ranks(a) -> int:
@@ -122,7 +136,8 @@ def main():
                      **({"batch_size": a.batch_size} if a.batch_size > 0 else {}),
                      **({"global_test_samples": a.global_test_samples}
                         if a.global_test_samples > 0 else {}),
-                     **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}))
+                     **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}),
+                     **_overrides(a.set))
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
         fed.run_round(r)
@@ -168,6 +183,8 @@ def main():
     multi = {}
     if rt.world > 1:
         ex = {"stale_rounds": [h.get("stale_rounds") for h in timed],
+              "stale_max": max([float(h.get("stale_max") or 0.0) for h in timed] or [0.0]),
+              "wait_s_total": sum(float(h.get("wait_s") or 0.0) for h in timed),
               "torn": sum(float(h.get("torn") or 0.0) for h in timed),
               "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
               "mixed": sum(float(h.get("mixed") or 0.0) for h in timed)}
@@ -239,9 +256,12 @@ def main():
                        "parallelism": f"fl{a.clients}-clients-on-{rt.world}gpu",
                        "clients": a.clients, "mode": a.mode,
                        "gossip": "sync" if a.sync else "async", "partition": cfg.partition,
-                       "gossip_mix": ("same-round snapshots (drift correction across ranks)"
-                                      if getattr(fed, "same_round_mix", False) else
-                                      "newest complete snapshot" if not a.sync else "same-round"),
+                       "gossip_mix": ("same-round snapshots (waits for every neighbour's "
+                                      "round-r post)" if getattr(fed, "same_round_mix", False) else
+                                      "same-round" if a.sync else
+                                      "newest complete snapshot, never waits" + (
+                                          " + exchanged SCAFFOLD control variates (stale-exact)"
+                                          if fed.drift.exchange else "")),
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
                        "client_lanes_per_gpu": len(fed.lanes) or 1,
                        "micro_batches_per_step": fed.micro_split,

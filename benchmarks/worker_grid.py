@@ -23,7 +23,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt: bool) -> dict:
+def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt: bool,
+        **extra) -> dict:
     import torch
     from bcfl.config import get_preset
     from bcfl.fl import Federation
@@ -34,7 +35,8 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
     cfg = get_preset("baseline3_learnable", mode=mode, model=model, num_clients=clients,
                      num_rounds=rounds, partition=part, train_samples=100, test_samples=100,
                      resample_each_round=(mode == "serverless"), out_dir=out_dir,
-                     reference_prints=False, save_every=1, keep_optimizer_state=keep_opt)
+                     reference_prints=False, save_every=1, keep_optimizer_state=keep_opt,
+                     **extra)
     fed = Federation(cfg, verbose=False)
     times = []
     for r in range(rounds):
@@ -55,7 +57,8 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
     fed.finish()
     steady = times[3:] if len(times) > 4 else times
     rec = {"mode": mode, "clients": clients, "rounds": rounds, "model": model,
-           "keep_optimizer_state": keep_opt,
+           "keep_optimizer_state": keep_opt, "overrides": extra,
+           "train_loss_curve": [h.get("train_loss") for h in fed.history],
            "s_per_round_steady": sum(steady) / len(steady), "total_rounds_s": sum(times),
            "process_latency_min": (time.time() - t_proc) / 60.0,
            "final_accuracy": fa.get("accuracy"), "global_eval_rows": fa.get("rows"),
@@ -81,7 +84,16 @@ def main(argv=None):
     ap.add_argument("--fresh-adamw", action="store_true",
                     help="the reference's fresh AdamW per round (oscillates on IID from random "
                          "init, profiles/accuracy_server_stability.json); default keeps moments")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra FLConfig override (JSON value), e.g. --set max_grad_norm=1.0")
     a = ap.parse_args(argv)
+    extra = {}
+    for it in a.set:
+        k, _, v = it.partition("=")
+        try:
+            extra[k.strip()] = json.loads(v)
+        except json.JSONDecodeError:
+            extra[k.strip()] = v
     res = {"reference": {"latency_min_server": [38, 41.8, 45.4], "latency_min_serverless": [27.8, 40, 41.5],
                          "acc_server": [68, 74, 80], "acc_serverless": [76, 83, 88],
                          "source": "All_graphs_IMDB_dataset.ipynb:747-748,830-831 (5/10/20 workers, 20 rounds, hardware unspecified, pretrained models)"},
@@ -89,7 +101,7 @@ def main(argv=None):
     for k in a.clients:
         for mode in a.modes:
             rec = one(mode, k, a.rounds, os.path.join("runs", "grid", f"{mode}{k}"), a.model,
-                      not a.fresh_adamw)
+                      not a.fresh_adamw, **extra)
             print(json.dumps({x: rec[x] for x in rec if x != "accuracy_curve"}), flush=True)
             res["runs"].append(rec)
             os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)

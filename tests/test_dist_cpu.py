@@ -316,3 +316,42 @@ def test_server_mailbox_equals_allreduce_when_all_live(tmp_path):
     b = run_world(_fed_worker, 2, str(tmp_path / "b"), "server", str(tmp_path / "b"), {})
     assert torch.equal(a[0]["master"], a[1]["master"])
     torch.testing.assert_close(a[0]["master"], b[0]["master"], atol=1e-6, rtol=0)
+
+
+def _server_lagging_worker(rank, world, out, delay_s):
+    import json as _json
+    import time as _time
+    from bcfl.fl import Federation
+    fed = Federation(_cfg("server", out, num_clients=2, num_rounds=10, server_transport="mailbox",
+                          server_timeout_s=1.0), verbose=False)
+    if rank == 1:
+        _time.sleep(delay_s)   # slow but alive: misses round 0's deadline of rank 0
+    fed.run()                  # a rank that joins a later epoch continues at that round
+    rounds = [b for b in fed.ledger.blocks() if b["kind"] == "global"]
+    pay = [_json.loads(b["payload"] or "{}") for b in rounds]
+    return {"G": fed.global_master.clone(),
+            "absent": [list(p.get("absent_ranks", [])) for p in pay],
+            "mismatch": [list(p.get("view_mismatch", [])) for p in pay],
+            "rejoined": [list(p.get("rejoined_ranks", [])) for p in pay],
+            "audit_checked": torch.tensor(fed.ledger_audit["checked"]),
+            "audit_mismatched": torch.tensor(fed.ledger_audit["mismatched"])}
+
+
+def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path):
+    """a rank that misses one deadline (slow, not dead) must not be excluded for good.
+    Rank 1 starts 1.5 s late: rank 0 times out on it (1 s) and aggregates alone for a few epochs;
+    rank 1 joins the federation's current epoch (the newest post it finds), where it still
+    receives rank 0's post and aggregates both — a split that the next posts' live-set words
+    expose (view_mismatch in the ledger). Rank 0 sees rank 1 posting again and waits for it, and
+    both ranks end on the bit-identical global model; every accepted receive matches its sender's
+    committed root in the cross-rank ledger audit."""
+    res = run_world(_server_lagging_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), 1.5)
+    r0, r1 = res
+    assert r0["absent"][0] == [1]                      # rank 0 timed out on the late rank 1
+    assert r1["absent"][0] == []                       # ... which joined rank 0's epoch
+    assert any(m for m in r0["mismatch"] + r1["mismatch"])   # the split is reported
+    assert any(r0["rejoined"]) or r0["absent"][-1] == []     # rank 1 came back
+    assert r0["absent"][-1] == [] and r1["absent"][-1] == []
+    assert torch.equal(r0["G"], r1["G"])               # same live set again -> same G
+    for r in res:
+        assert int(r["audit_checked"]) > 0 and int(r["audit_mismatched"]) == 0

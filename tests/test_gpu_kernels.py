@@ -709,3 +709,39 @@ def test_embedding_grads_with_host_sort_order_are_identical():
         outs.append(torch.autograd.grad(y, (word, posw, typ, g, be), go))
     for a, c in zip(*outs):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("with_g2", [False, True])
+def test_grad_clip_coef_and_clipped_adamw(with_g2):
+    """Fused global-norm clipping (FLConfig.max_grad_norm): the multi-tensor norm kernel equals
+    the fp64 norm of the concatenated gradients, the coefficient is torch's clip_grad_norm_
+    (min(1, max / (norm + 1e-6))), and adamw_mt with the device coefficient equals AdamW on the
+    clipped gradients — with no host read in between."""
+    torch.manual_seed(1)
+    sizes = [768, 3, 3072 * 768, 5, 777] + [129] * 45
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    grads = [torch.randn(n, device=DEV).bfloat16() for n in sizes]
+    g2 = [torch.randn(n, device=DEV).bfloat16() for n in sizes] if with_g2 else None
+    full = [g.double() + (g2[i].double() if g2 else 0) for i, g in enumerate(grads)]
+    norm = float(torch.cat(full).norm())
+    for max_norm in (norm * 0.25, norm * 4):
+        c = ops.grad_clip_coef(grads, max_norm, g2)
+        assert c.is_cuda and c.dtype == torch.float32
+        assert float(c[1]) == pytest.approx(norm, rel=1e-5)
+        assert float(c[0]) == pytest.approx(min(1.0, max_norm / (norm + 1e-6)), rel=1e-5)
+    c = ops.grad_clip_coef(grads, norm * 0.25, g2)
+    master = torch.randn(o, device=DEV)
+    m, v = torch.zeros(o, device=DEV), torch.zeros(o, device=DEV)
+    rm, rmm, rvv = master.clone(), m.clone(), v.clone()
+    ops.adamw_multi_(master, grads, offs, m, v, 1, 1e-3, 0.9, 0.999, 1e-6, 0.0, "hf",
+                     grads2=g2, gscale=c)
+    k = float(c[0])
+    for gf, of in zip(full, offs):
+        n = gf.numel()
+        ref.adamw_(rm[of:of + n], (gf * k).float(), rmm[of:of + n], rvv[of:of + n], 1, 1e-3, 0.9,
+                   0.999, 1e-6, 0.0, "hf")
+    _close(m, rmm, 1e-6, 1e-5)
+    _close(master, rm, 1e-5, 1e-5)

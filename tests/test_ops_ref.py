@@ -148,3 +148,27 @@ def test_merkle_root_host():
     if native_available():
         from bcfl import _host
         assert _host.merkle_root_hex(buf.numpy(), leaf) == merkle_from_leaves(leaves).hex()
+
+
+def test_flat_adamw_clipping_matches_torch_clip_grad_norm():
+    """FlatAdamW(max_grad_norm) == torch.nn.utils.clip_grad_norm_ + the same AdamW step (CPU
+    reference path; the GPU kernel is pinned in tests/test_gpu_kernels.py)."""
+    import torch
+    from bcfl.parallel.flat import FlatAdamW, FlatParams
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(37, 5)), torch.nn.Parameter(torch.randn(11))]
+    flat = FlatParams(ps, "cpu", torch.float32)
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FlatAdamW(flat, lr=1e-2, mode="torch", max_grad_norm=0.5)
+    ropt = torch.optim.AdamW(ref_ps, lr=1e-2, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.0)
+    for _ in range(3):
+        gs = [torch.randn_like(p) * 3 for p in ps]
+        for p, q, g in zip(ps, ref_ps, gs):
+            p.grad, q.grad = g.clone(), g.clone()
+        tn = torch.nn.utils.clip_grad_norm_(ref_ps, 0.5)
+        opt.step()
+        ropt.step()
+        assert float(opt.last_grad_norm) == pytest.approx(float(tn), rel=1e-5)
+        flat.zero_grad()
+    for p, q in zip(ps, ref_ps):
+        torch.testing.assert_close(p.detach(), q.detach(), atol=1e-6, rtol=1e-5)

@@ -162,9 +162,15 @@ def _infopass_cpu_worker(rank, world):
     from bcfl.parallel import dist as D
     from bcfl.trust.infopass import measure
     D.init_runtime("cpu", "gloo")
+    from bcfl.trust.infopass import summary
     r = measure(1 << 16, iters=2)
+    dets = r["detectors"]
     return {"n": torch.tensor(len(r["sources"])), "bw": torch.tensor(r["bw_MBps"]),
-            "pred": torch.tensor([s.get("predicted_async_s", -1.0) for s in r["sources"]])}
+            "pred": torch.tensor([s.get("predicted_async_s", -1.0) for s in r["sources"]]),
+            "bcfl": torch.tensor([[s["bcfl"]["sync_s"], s["bcfl"]["async_s"], s["measured_sync_s"],
+                                   s["bcfl"]["commit_s"]] for s in r["sources"]]),
+            "dets": sorted(dets), "lines": len(summary(r)),
+            "det_rows": sum(len(e["sources"]) for e in dets.values())}
 
 
 def test_info_passing_mailbox_gloo(tmp_path):
@@ -178,3 +184,9 @@ def test_info_passing_mailbox_gloo(tmp_path):
     bw = r["bw"]
     assert bool((bw[~torch.eye(3, dtype=torch.bool)] > 0).all())
     assert bool((r["pred"] > 0).all())
+    # BC-FL: commitment on send + re-hash on receive, on top of the plain posts
+    b = r["bcfl"]
+    assert bool((b > 0).all()) and bool((b[:, 0] >= b[:, 3]).all())
+    # all three reference detectors, each with its own re-measured rows (or the skip reason)
+    assert r["dets"] == ["dbscan", "modz", "pagerank"] and r["det_rows"] == 9
+    assert r["lines"] == 3 + 9
