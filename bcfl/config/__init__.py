@@ -85,6 +85,12 @@ class FLConfig:
                                             # neighbour view to the present in the mix — "own":
                                             # + k * (this client's own update of the round),
                                             # "global": - k * L * c_hat (fl/drift.py)
+    gossip_exchange: str = "auto"       # mailbox gossip payload: "state" (models, mixed as states)
+                                        # | "delta" (cumulative own updates, each applied once:
+                                        # async FedAvg, no pull-back to stale states) | auto =
+                                        # delta for multi-rank async gossip on complete graphs
+    gossip_apply_on_arrival: bool = True  # delta exchange: apply neighbours' updates between
+                                          # local steps as they arrive (non-blocking polls)
     gossip_stale_decay: float = 0.0     # async mailbox mix: a view k rounds behind keeps
                                         # W / (1 + decay * k) of its weight (rest -> self)
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
@@ -165,6 +171,7 @@ class FLConfig:
                    "server_transport": ("rccl", "mailbox"),
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
                    "drift_exchange": ("auto", "on", "off"),
+                   "gossip_exchange": ("auto", "state", "delta"),
                    "drift_stale_compensation": ("none", "own", "global"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),

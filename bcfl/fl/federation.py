@@ -143,6 +143,7 @@ class Federation:
         if cfg.compat_chain and self.rt.world > 1:
             raise ValueError("compat_chain reproduces the reference's single-process chain; world must be 1")
         self.client_rng = {c: {"seed": _cseed(cfg.seed, c), "counter": 0} for c in self.local_clients}
+        self._phase: Dict[int, str] = {}   # hosted client -> "training" / "trained" this round
         self.client_opt: Dict[int, dict] = {}
         self.client_master: Dict[int, torch.Tensor] = {}
         if cfg.mode == "serverless" and self.multi and not cfg.compat_chain:
@@ -218,6 +219,16 @@ class Federation:
                       else {self.local_clients[0]: self.flat.master})
             if self.transport == "mailbox":
                 aux = self.drift.use_exchange() if cv_exchange else None
+                exch = cfg.gossip_exchange
+                if exch == "auto":
+                    # delta exchange where snapshots can be stale: several ranks, async, and a
+                    # complete neighbour graph (applying every update once needs everyone's)
+                    exch = ("delta" if (self.rt.distributed and cfg.async_gossip
+                                        and not self.same_round_mix
+                                        and cfg.topology in ("full", "pagerank")) else "state")
+                if exch == "delta" and cfg.topology == "ring":
+                    raise ValueError("gossip_exchange='delta' applies each client's updates once "
+                                     "and needs a complete topology (full / pagerank), not ring")
                 try:
                     self.gossip = MailboxGossip(n, states, self.nbrs,
                                                 "fp32" if cfg.wire_dtype == "fp32" else "bf16",
@@ -228,7 +239,8 @@ class Federation:
                                                 sync_timeout_s=10.0 if self.same_round_mix else 60.0,
                                                 liveness_timeout=cfg.liveness_timeout,
                                                 verify=cfg.verify_updates, aux=aux,
-                                                aux_sink=self.drift if aux else None)
+                                                aux_sink=self.drift if aux else None,
+                                                exchange=exch)
                     self.drift.stale_compensation = cfg.drift_stale_compensation
                     self.gossip.stale_decay = float(cfg.gossip_stale_decay)
                 except MailboxUnavailable as e:
@@ -250,6 +262,11 @@ class Federation:
                 self.gossip = GossipEngine(n, states, self.nbrs, wire, rccl_async,
                                            liveness_timeout=cfg.liveness_timeout,
                                            verify=cfg.verify_updates)
+            if isinstance(self.gossip, MailboxGossip):
+                # apply on arrival: neighbours' updates enter between local steps (delta exchange)
+                self.gossip.W_mid = mixing_matrix(self.nbrs, cfg.mixing)
+                self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival)
+                self.gossip._also = self._mid_round_targets
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
             self.gossip.tamper = set(cfg.inject_tamper) & set(self.local_clients)
             self.gossip.seed_replicas(self.flat.master)
@@ -363,6 +380,30 @@ class Federation:
     def _on(self, lane: ClientLane):
         return torch.cuda.stream(lane.stream) if lane.stream is not None else contextlib.nullcontext()
 
+    def _mark_start(self, c: int, master: torch.Tensor) -> None:
+        self._phase[c] = "training"
+        g = getattr(self, "gossip", None)
+        if g is not None and hasattr(g, "mark_start"):
+            g.mark_start(c, master)
+
+    def _mid_round_targets(self, c: int) -> List[torch.Tensor]:
+        """Buffers that follow a hosted client's model when a neighbour's update is applied
+        mid-round: the drift correction's round-start copy while the client trains."""
+        if self.drift.exchange and self._phase.get(c) == "training":
+            return [self.drift.cv[c]]
+        return []
+
+    def _gossip_poll(self) -> None:
+        """Between local steps: let arrived neighbour updates in (non-blocking)."""
+        g = self.gossip
+        if not isinstance(g, MailboxGossip) or not g.apply_on_arrival:
+            return
+        if self.lanes:
+            streams = {c: ln.stream for ln in self.lanes for c in ln.clients}
+            g.poll(streams, self.client_param, self._mid_round_targets)
+        else:
+            g.poll(None, {self.local_clients[0]: self.flat.param}, self._mid_round_targets)
+
     @contextlib.contextmanager
     def _client_rng(self, c: int):
         g = ops.rng.global_rng()
@@ -384,6 +425,7 @@ class Federation:
                 else:
                     lane.opt.reset()
                 self.drift.attach(lane.opt, c, lane.flat.master)
+                self._mark_start(c, lane.flat.master)
                 prev = lane.flat.master.detach().clone() if need_prev else None
                 loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
             st = {"batches": 0, "tokens": 0, "examples": 0}
@@ -410,6 +452,7 @@ class Federation:
                 time.sleep(cfg.inject_slow[c] / 1000.0)
             with self._on(lane):
                 self.drift.after_train(c, lane.flat.master, self.lr_sum(r, st["batches"]))
+                self._phase[c] = "trained"
                 self.drift.detach(lane.opt)
                 if prev is not None:
                     self._inject_byzantine(c, prev, lane.flat)
@@ -440,6 +483,7 @@ class Federation:
                         next(g)
                     except StopIteration:
                         gens.remove(g)
+                self._gossip_poll()
             # the join is part of the phase: its device end event then covers every lane
             for ln in self.lanes:
                 if ln.stream is not None:
@@ -731,6 +775,7 @@ class Federation:
         else:
             self.opt.reset()
         self.drift.attach(self.opt, c, self.flat.master)
+        self._mark_start(c, self.flat.master)
         ops.rng.global_rng().load_state(self.client_rng[c])
 
     def _deactivate(self, c: int):
@@ -749,7 +794,8 @@ class Federation:
                 batches = self.train_batches(c, r, e)
             with self.timer.phase("train"):
                 res = self.trainer.train_epoch(
-                    batches, lr_fn=lambda i, e=e: self.lr_at(r, e * len(batches) + i))
+                    batches, lr_fn=lambda i, e=e: self.lr_at(r, e * len(batches) + i),
+                    step_hook=self._gossip_poll if self.cfg.mode == "serverless" else None)
             loss_t = res["loss_sum"] if loss_t is None else loss_t + res["loss_sum"]
             for k in ("batches", "tokens", "examples"):
                 out[k] += res[k]
@@ -1124,6 +1170,7 @@ class Federation:
             prev = self.flat.master.detach().clone() if need_prev else None
             st = self._train_client(c, r)
             self.drift.after_train(c, self.flat.master, self.lr_sum(r, st["batches"]))
+            self._phase[c] = "trained"
             self.drift.detach(self.opt)
             if prev is not None:
                 self._inject_byzantine(c, prev)
@@ -1145,6 +1192,8 @@ class Federation:
         # async mixes states published last round -> apply last round's verdicts to them
         use_v = self.prev_verdicts if (cfg.async_gossip and not self.same_round_mix) else v
         W = mixing_matrix(self.nbrs, cfg.mixing, use_v.rejected)
+        if isinstance(self.gossip, MailboxGossip):
+            self.gossip.W_mid = W
         with self.timer.phase("comm"):
             pout = (self.client_param if self.lanes else
                     None if self.multi else {self.local_clients[0]: self.flat.param})

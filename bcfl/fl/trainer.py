@@ -102,12 +102,17 @@ class LocalTrainer:
         self.flat.zero_grad()
         loss_acc += loss.detach()
 
-    def train_epoch(self, batches: Sequence[PackedBatch], lr_fn=None) -> Dict[str, torch.Tensor]:
+    def train_epoch(self, batches: Sequence[PackedBatch], lr_fn=None,
+                    step_hook=None) -> Dict[str, torch.Tensor]:
+        """``step_hook()`` runs after every optimizer step (async gossip: neighbours' updates
+        that have arrived are applied between local steps)."""
         loss_acc = torch.zeros((), dtype=torch.float32, device=self.flat.device)
         for i, b in enumerate(batches):
             if lr_fn is not None:
                 self.opt.lr = lr_fn(i)
             self.step(b, loss_acc)
+            if step_hook is not None:
+                step_hook()
         return {"loss_sum": loss_acc, "batches": len(batches),
                 "tokens": sum(b.real_tokens for b in batches),
                 "examples": sum(b.batch_size for b in batches)}

@@ -360,6 +360,17 @@ class MailboxGossip:
     round r (or ``sync_timeout_s`` passes and it is declared dead) — lock-step semantics without
     any matched transfer, for the sync-vs-async comparison.
 
+    ``exchange="delta"`` (complete topologies, asynchronous FedAvg semantics): instead of its
+    model state, every client publishes the CUMULATIVE sum of its own local updates,
+    ``S_c = sum_r (y_c^r - x_c^r)``, and a receiver adds each neighbour's NEW progress
+    ``S_j^new - S_j^applied`` exactly once: ``x_c <- y_c - (1 - W_cc) u_c + sum_j W_cj dS_j``.
+    A stale snapshot then only delays a neighbour's update by a round — it never pulls the mix
+    back to an old state, which is what state mixing with stale snapshots does (2 / 4 ranks on
+    one MI355X stayed at the majority rate, profiles/multirank_async_r4.json). Under exact
+    same-round mixing both forms give the reference's mean of the trained models. Lost, torn or
+    rejected versions are harmless: the next good snapshot's difference covers them, and the
+    bf16 rounding of ``S_j`` telescopes (only the newest snapshot's rounding is ever present).
+
     ``aux`` (optional, per hosted client, fp32, same size as the model): a second state published
     in the SAME payload (``[model | aux]``, one version, one header, one Merkle commitment) — the
     clients' SCAFFOLD control variates (:mod:`bcfl.fl.drift`, exchange mode). ``aux_sink`` (the
@@ -374,7 +385,7 @@ class MailboxGossip:
                  wire: str = "bf16", sync: bool = False, liveness_timeout: int = 2,
                  verify: bool = True, sync_timeout_s: float = 60.0, rank: Optional[int] = None,
                  world: Optional[int] = None, aux: Optional[Dict[int, torch.Tensor]] = None,
-                 aux_sink=None):
+                 aux_sink=None, exchange: str = "state"):
         from .mailbox import MailboxTransport
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
@@ -426,18 +437,145 @@ class MailboxGossip:
         self._round_local = -1
         self.wait_s = 0.0              # host time spent waiting for peers (sync mode only)
         self.stale_decay = 0.0         # see _age_weighted
+        if exchange not in ("state", "delta"):
+            raise ValueError(f"exchange must be 'state' or 'delta', got {exchange!r}")
+        self.exchange = exchange
+        self._fresh: Dict[int, object] = {}
+        if exchange == "delta":
+            f32 = lambda: torch.zeros(self.numel, dtype=torch.float32, device=self.device)  # noqa: E731
+            self.start = {c: f32() for c in self.local}   # round-start model, then u_c
+            self.cum = {c: f32() for c in self.local}     # S_c, the published quantity
+        # apply on arrival (delta exchange, async): mixing weights for mid-round application,
+        # the in-flight non-blocking fetch, the events of the last applications (the next fetch
+        # may overwrite the buffers they read only after them), hosted clients whose round began
+        self.apply_on_arrival = exchange == "delta" and not sync
+        self._also = None              # callback c -> extra buffers updated with mid-round deltas
+        self.W_mid: Optional[np.ndarray] = None
+        self._inflight = None
+        self._apply_events: List = []
+        self._started: set = set()
+        self.applied_mid = 0
 
     # ------------------------------------------------------------------------------------
     def seed_replicas(self, initial: torch.Tensor):
         """Every client starts from the identical initial model, so every replica (version 0)
         starts equal to it: a neighbour that never publishes is mixed as the initial model until
-        the staleness bound retires it. Aux halves (control variates) start at zero."""
+        the staleness bound retires it (delta exchange: version 0 = no progress, S = 0). Aux
+        halves (control variates) start at zero."""
         n = self.numel
         for t in [self.replica[j] for j in self.remote_needed] + \
                  [b for c in self.local for b in self.send_buf[c]]:
-            ops.cast_copy_(t[:n], initial)
+            if self.exchange == "delta":
+                t[:n].zero_()
+            else:
+                ops.cast_copy_(t[:n], initial)
             if self.aux is not None:
                 t[n:].zero_()
+        if self.exchange == "delta":
+            for c in self.local:
+                self.cum[c].zero_()
+
+    def mark_start(self, c: int, x: torch.Tensor) -> None:
+        """Delta exchange: record hosted client c's round-start model (stream-ordered before its
+        first optimizer step); its update u_c = y_c - x_c is formed at publish."""
+        if self.exchange == "delta":
+            self.start[c].copy_(x)
+            self._started.add(c)
+
+    # ---- apply on arrival ---------------------------------------------------------------------
+    def _hash(self, t: torch.Tensor):
+        return ops.merkle_root_deferred(t)
+
+    @torch.no_grad()
+    def poll(self, streams: Optional[Dict[int, object]] = None,
+             param_out: Optional[Dict[int, torch.Tensor]] = None, also=None) -> int:
+        """Asynchronous gossip overlapped with local training (delta exchange): NON-BLOCKING.
+        Advances the in-flight fetch by one step (header read -> payload copy, seqlock re-read
+        and receiver re-hash on the fetch stream -> host checks, each step only an event query);
+        when its snapshots are complete and verified, every hosted client c gets each fresh
+        neighbour's new progress ``W_cj (S_j^new - S_j^applied)`` added to its model (on c's own
+        lane stream, after the fetch; ``param_out[c]`` refreshed in the same kernel), to its
+        round-start record if its round has begun (u_c stays its own progress) and to the
+        buffers ``also(c)`` returns; then the next fetch starts. Called between local steps, so
+        a neighbour's update enters a round or more earlier than at the round's end mix.
+        Returns the number of snapshots applied."""
+        if not (self.apply_on_arrival and self.remote_needed) or self.W_mid is None:
+            return 0
+        tr = self.transport
+        h = self._inflight
+        if h is None:
+            md = getattr(self, "_mix_done", None)   # the round-end mix read stage / replica too
+            self._inflight = tr.fetch_begin({j: self.applied[j] for j in self.remote_needed},
+                                            self.stage,
+                                            after=self._apply_events + ([md] if md is not None else []))
+            self._apply_events = []
+            h = self._inflight
+        res = tr.fetch_advance(h, self._hash if self.verify else None)
+        if res is None:
+            return 0
+        self._inflight = None
+        return self._apply_fetched(res, h, streams, param_out, also)
+
+    @torch.no_grad()
+    def _finish_inflight(self, param_out=None, also=None) -> int:
+        """Complete an in-flight fetch (blocking) and apply it on the current stream."""
+        h, self._inflight = self._inflight, None
+        if h is None:
+            return 0
+        res = self.transport.fetch_wait(h, self._hash if self.verify else None)
+        return self._apply_fetched(res, h, None, param_out, also)
+
+    def _apply_fetched(self, res, h, streams, param_out, also) -> int:
+        if not res:
+            return 0
+        self.torn = self.transport.torn
+        good = {}
+        for j, snap in res.items():
+            if self.verify:
+                got = h.roots.get(j)
+                if got is None:   # CPU path: the fetch was synchronous, hash here
+                    got = ops.root_bytes(ops.merkle_root_deferred(self.stage[j]))
+                ok = got == snap.root
+            else:
+                ok = True
+            self.records.append({"client": j, "kind": "recv", "version": snap.version,
+                                 "root": snap.root.hex(), "ok": ok, "src_round": snap.round})
+            if not ok:
+                self.rejected_msgs += 1
+                continue
+            good[j] = snap
+        if not good:
+            return 0
+        n, W = self.numel, self.W_mid
+        cuda = self.transport.is_cuda
+        for c in self.local:
+            views, ws = [], []
+            for j in good:
+                if W[c, j] != 0.0:
+                    views += [self.stage[j][:n], self.replica[j][:n]]
+                    ws += [float(W[c, j]), -float(W[c, j])]
+            if not views:
+                continue
+            st = (streams or {}).get(c) if cuda else None
+            cur = st if st is not None else (torch.cuda.current_stream(self.device) if cuda else None)
+            with (torch.cuda.stream(cur) if cuda else _nullctx()):
+                if cuda and h.done_event is not None:
+                    cur.wait_event(h.done_event)
+                ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
+                if c in self._started:
+                    ops.gossip_mix_(self.start[c], views, 1.0, ws)
+                for t in (also(c) if also is not None else []):
+                    ops.gossip_mix_(t, views, 1.0, ws)
+                if cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    self._apply_events.append(ev)
+        for j, snap in good.items():
+            self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
+            self.applied[j] = snap.version
+            self.replica_round[j] = snap.round
+        self.applied_mid += len(good)
+        return len(good)
 
     def _msg(self, j: int) -> torch.Tensor:
         if j in self.states:
@@ -449,13 +587,21 @@ class MailboxGossip:
         return self._msg(j)[: self.numel]
 
     def aux_view(self, j: int) -> torch.Tensor:
-        """Newest verified aux state (control variate) of client j, same version as :meth:`view`."""
+        """Newest verified aux state (control variate) of client j, same version as :meth:`view`
+        (delta exchange: a snapshot fetched this round is still in the staging buffer)."""
+        if j in self._fresh:
+            return self.stage[j][self.numel:]
         return self._msg(j)[self.numel:]
 
     @torch.no_grad()
     def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None):
         from .mailbox import Snapshot
         roots = {}
+        if self.exchange == "delta":
+            for c in self.local:   # u_c = y_c - x_c (in place), S_c += u_c
+                ops.axpby_(self.start[c], self.states[c], 1.0, -1.0)
+                ops.axpby_(self.cum[c], self.start[c], 1.0, 1.0)
+            self._started = set()
         for c in self.local:
             if c in self.suppressed:
                 continue
@@ -465,7 +611,8 @@ class MailboxGossip:
             if self.transport.is_cuda:
                 self.transport.wait_slot_free(c, slot)
             buf = self.send_buf[c][slot]
-            ops.cast_copy_(buf[: self.numel], self.states[c])
+            ops.cast_copy_(buf[: self.numel],
+                           self.cum[c] if self.exchange == "delta" else self.states[c])
             if self.aux is not None:
                 ops.cast_copy_(buf[self.numel:], self.aux[c])
             roots[c] = ops.merkle_root_deferred(buf) if self.verify else None
@@ -491,6 +638,10 @@ class MailboxGossip:
         tr = self.transport
         fs = tr.fetch_stream  # GPU: the whole receive path runs on the transport's side stream
         after = getattr(self, "_mix_done", None)
+        if fs is not None:
+            for ev in self._apply_events:   # mid-round applications read stage / replica
+                fs.wait_event(ev)
+            self._apply_events = []
         got = tr.fetch(want, self.stage, after=after)
         if not self.async_gossip:
             t0 = _time.perf_counter()
@@ -524,7 +675,10 @@ class MailboxGossip:
             if not good:
                 self.rejected_msgs += 1
                 continue
-            self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
+            if self.exchange == "delta":
+                self._fresh[j] = snap   # applied (S_new - S_applied) by the mix, then swapped
+            else:
+                self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
             self.applied[j] = snap.version
             self.replica_round[j] = snap.round
 
@@ -540,6 +694,42 @@ class MailboxGossip:
 
     def live_matrix(self, W: np.ndarray) -> np.ndarray:
         return GossipEngine.live_matrix(self, W)
+
+    @torch.no_grad()
+    def mix_delta(self, W: np.ndarray, round_idx: int,
+                  param_out: Optional[Dict[int, torch.Tensor]] = None,
+                  extra: Optional[Dict[int, list]] = None):
+        """x_c <- y_c - (1 - W_cc) u_c + sum_{j local} W_cj u_j
+                   + sum_{j remote, new snapshot} a_j W_cj (S_j^new - S_j^applied)  (one kernel)
+
+        ``a_j = 1 / (1 + stale_decay * max(0, tau_j - 1))`` with tau_j the rounds the snapshot is
+        behind: the usual one-round async lag is applied in full, updates computed on a model
+        several rounds old are damped (FedAsync-style staleness weighting)."""
+        n = self.numel
+        damp = {}
+        for j, snap in self._fresh.items():
+            tau = max(0, round_idx - snap.round)
+            damp[j] = 1.0 / (1.0 + self.stale_decay * max(0, tau - 1))
+        for c in self.local:
+            views = [self.start[c]]
+            ws = [-(1.0 - float(W[c, c]))]
+            for j in range(self.n):
+                if j == c or W[c, j] == 0.0:
+                    continue
+                if j in self.states:
+                    views.append(self.start[j])
+                    ws.append(float(W[c, j]))
+                elif j in self._fresh:
+                    wj = float(W[c, j]) * damp[j]
+                    views += [self.stage[j][:n], self.replica[j][:n]]
+                    ws += [wj, -wj]
+            for t, wt in ((extra or {}).get(c) or []):
+                views.append(t)
+                ws.append(float(wt))
+            ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
+        for j in list(self._fresh):   # the new snapshot becomes the applied one
+            self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
+        self._fresh = {}
 
     def _age_weighted(self, W: np.ndarray, round_idx: int) -> np.ndarray:
         """``stale_decay`` > 0: a neighbour view k rounds behind keeps W_cj / (1 + decay * k) of
@@ -567,13 +757,19 @@ class MailboxGossip:
                      param_out: Optional[Dict[int, torch.Tensor]] = None,
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
         b0, w0 = self.transport.bytes_posted, self.wait_s
+        if self._inflight is not None:
+            # the round's training is done: complete the mid-round fetch before publishing (its
+            # applications must land in the clients' start records before u_c is formed)
+            self._finish_inflight(param_out, self._also)
         self.publish(round_idx, steps)
         self.collect(round_idx)
         self._age_out(round_idx)
         fs = self.transport.fetch_stream
         if fs is not None:  # the mix reads what the fetch stream wrote
             torch.cuda.current_stream(self.device).wait_stream(fs)
-        Wl = self._age_weighted(self.live_matrix(W), round_idx)
+        Wl = self.live_matrix(W)
+        if self.exchange != "delta":
+            Wl = self._age_weighted(Wl, round_idx)
         extra = {}
         if self.aux is not None and self.aux_sink is not None:
             for c in self.local:
@@ -582,7 +778,12 @@ class MailboxGossip:
                           for j in nb if j not in self.states)
                 extra[c] = self.aux_sink.begin(c, float(Wl[c, c]), [self.aux_view(j) for j in nb],
                                                [float(Wl[c, j]) for j in nb], age)
-        self.mix(Wl, param_out, extra)
+        if self.exchange == "delta":
+            # updates are applied once with the topology's weights (a silent neighbour simply
+            # contributes no new progress); the live weights above form c_hat
+            self.mix_delta(W, round_idx, param_out, extra)
+        else:
+            self.mix(Wl, param_out, extra)
         if self.aux is not None and self.aux_sink is not None:
             for c in self.local:
                 self.aux_sink.end(c)
@@ -598,6 +799,8 @@ class MailboxGossip:
                 "rejected_msgs": float(self.rejected_msgs)}
 
     def drain(self):
+        if self._inflight is not None and self._inflight.done_event is not None:
+            self._inflight.done_event.synchronize()   # no fetch left writing into stage[]
         self.transport.drain()
 
     def close(self):
@@ -611,8 +814,11 @@ class MailboxGossip:
         """Published snapshots, verified replicas, versions and liveness. Inbox contents are NOT
         state: after a restart peers simply post again (a replica's version tells what is new)."""
         self.drain()
+        self._inflight = None          # an unapplied mid-round fetch is simply fetched again
         t = lambda d: {int(k): v.detach().cpu().clone() for k, v in d.items()}  # noqa: E731
-        return {"send_buf": {int(c): [b.detach().cpu().clone() for b in v] for c, v in self.send_buf.items()},
+        st = {"cum": t(self.cum)} if self.exchange == "delta" else {}
+        return {**st,
+                "send_buf": {int(c): [b.detach().cpu().clone() for b in v] for c, v in self.send_buf.items()},
                 "replica": t(self.replica), "version": dict(self.version), "steps": dict(self.steps),
                 "applied": dict(self.applied), "replica_round": dict(self.replica_round),
                 "dead": sorted(self.dead), "rejected_msgs": self.rejected_msgs,
@@ -624,6 +830,9 @@ class MailboxGossip:
                 dst.copy_(src.to(dst.device))
         for j, v in st["replica"].items():
             self.replica[int(j)].copy_(v.to(self.replica[int(j)].device))
+        if self.exchange == "delta" and "cum" in st:
+            for c, v in st["cum"].items():
+                self.cum[int(c)].copy_(v.to(self.device))
         for name in ("version", "steps", "applied", "replica_round"):
             getattr(self, name).update({int(k): int(v) for k, v in st[name].items()})
         self.dead = set(int(x) for x in st["dead"])

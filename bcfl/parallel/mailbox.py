@@ -413,8 +413,111 @@ class MailboxTransport:
             torch.cuda.current_stream(self.device).wait_stream(fs)
         return good
 
+    # ---------------------------------------------------------- non-blocking receive
+    def fetch_begin(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
+                    after: Sequence["torch.cuda.Event"] = ()) -> "AsyncFetch":
+        """Start a NON-BLOCKING fetch (GPU): the header read is queued on the fetch stream into
+        pinned host memory and nothing waits; :meth:`fetch_advance` moves it on when its event
+        has completed. ``after``: events after which the ``out`` buffers are free (their last
+        readers). CPU: completes synchronously (the shared-memory copies are host copies)."""
+        h = AsyncFetch(want, out)
+        if not self.is_cuda:
+            h.result = self.fetch(want, out)
+            return h
+        fs = self.fetch_stream
+        for ev in after:
+            fs.wait_event(ev)
+        js = list(want)
+        if not js:
+            h.result = {}
+            return h
+        with torch.cuda.stream(fs):
+            dev = torch.stack([self.inbox[j].hdr for j in js])
+            h.hdr = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+            h.hdr.copy_(dev, non_blocking=True)
+            h.ev = torch.cuda.Event()
+            h.ev.record(fs)
+        h.js = js
+        return h
+
+    def fetch_advance(self, h: "AsyncFetch", hash_fn=None) -> Optional[Dict[int, Snapshot]]:
+        """Advance a non-blocking fetch by one step if its queued work has completed; returns
+        the validated snapshots when done (``None`` while pending). Step 1: pick every inbox with
+        a complete version newer than wanted, queue its payload copy, the seqlock re-read of its
+        header and (``hash_fn``) the receiver's re-hash, all on the fetch stream. Step 2: drop
+        torn copies; ``h.roots[j]`` holds the receiver-side root bytes."""
+        if h.result is not None:
+            return h.result
+        if not h.ev.query():
+            return None
+        fs = self.fetch_stream
+        if h.step == 1:
+            first = h.hdr.numpy()
+            picked = {}
+            for i, j in enumerate(h.js):
+                nw = self.newest(first[i])
+                if nw is not None and nw[1].version > h.want[j]:
+                    picked[j] = nw
+            if not picked:
+                h.result = {}
+                return h.result
+            pj = list(picked)
+            with torch.cuda.stream(fs):
+                for j in pj:
+                    h.out[j].copy_(self.inbox[j].slots[picked[j][0]], non_blocking=True)
+                dev = torch.stack([self.inbox[j].hdr for j in pj])
+                h.hdr2 = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+                h.hdr2.copy_(dev, non_blocking=True)
+                if hash_fn is not None:
+                    rts = [hash_fn(h.out[j]) for j in pj]
+                    h.root_host = torch.empty((len(pj), 32), dtype=torch.uint8, pin_memory=True)
+                    h.root_host.copy_(torch.stack([r.view(torch.uint8).reshape(32) for r in rts]),
+                                      non_blocking=True)
+                h.ev = torch.cuda.Event()
+                h.ev.record(fs)
+            h.picked, h.pj, h.step = picked, pj, 2
+            return None
+        second = h.hdr2.numpy()
+        good = {}
+        for i, j in enumerate(h.pj):
+            slot, snap = h.picked[j]
+            if int(second[i][slot, W_BEGIN]) == snap.version and int(second[i][slot, W_END]) == snap.version:
+                good[j] = snap
+                if h.root_host is not None:
+                    h.roots[j] = bytes(h.root_host[i].numpy().tobytes())
+            else:
+                self.torn += 1
+        h.result = good
+        return good
+
+    def fetch_wait(self, h: "AsyncFetch", hash_fn=None) -> Dict[int, Snapshot]:
+        """Drive a non-blocking fetch to completion (blocking on its events)."""
+        while True:
+            r = self.fetch_advance(h, hash_fn)
+            if r is not None:
+                return r
+            h.ev.synchronize()
+
     def close(self):
         self.drain()
         self.outbox.clear()
         self.inbox.clear()
         self.backend.close()
+
+
+class AsyncFetch:
+    """Handle of a non-blocking mailbox fetch (:meth:`MailboxTransport.fetch_begin`)."""
+
+    def __init__(self, want: Dict[int, int], out: Dict[int, torch.Tensor]):
+        self.want, self.out = dict(want), out
+        self.result: Optional[Dict[int, Snapshot]] = None
+        self.step = 1
+        self.ev = None
+        self.js: List[int] = []
+        self.hdr = self.hdr2 = self.root_host = None
+        self.roots: Dict[int, bytes] = {}
+
+    @property
+    def done_event(self):
+        """Event after the fetch's last queued device work (None on CPU / when nothing ran)."""
+        return self.ev

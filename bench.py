@@ -237,6 +237,8 @@ def main():
                 "the global model on the draw" if cfg.mode == "server" else
                 "each rank's first client model on the draw (rank 0 reported)"),
             "final_majority_rate": last.get("global_majority_rate"),
+            "accuracy_curve": [round(float(x), 4) for x in fed.global_accuracies],
+            "accuracy_curve_scope": "rank 0's hosted client models on their strides of the draw, per round",
             "global_eval_rows": last.get("global_eval_rows"),
             "final_train_loss": last.get("train_loss"),
             "baseline_final_accuracy": BASELINE_FINAL_ACC,

@@ -380,3 +380,51 @@ def test_server_lanes_match_sequential(tmp_out, lanes):
     assert [h["global_acc"] for h in ha] == [h["global_acc"] for h in hb]
     # Flower's evaluate_round on the lanes: every client scores the same global model
     assert [h["distributed_acc"] for h in ha] == [h["distributed_acc"] for h in hb]
+
+
+def _one_rank_run(tmp_path, tag, **kw):
+    import torch
+    from bcfl.config import get_preset
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(2)
+    try:
+        cfg = get_preset("baseline3_learnable", model="tiny-bert", num_clients=4, num_rounds=3,
+                         mode="serverless", lr=2e-3, lr_warmup_steps=4, max_seq_len=64,
+                         train_samples=64, global_test_samples=40, eval_local=False,
+                         save_every=0, ledger=False, device="cpu", reference_prints=False,
+                         out_dir=str(tmp_path / tag), gossip_transport="mailbox",
+                         wire_dtype="fp32", dropout=0.0, **kw)
+        fed = Federation(cfg, verbose=False)
+        fed.run()
+        return fed
+    finally:
+        torch.set_num_threads(nt)
+        D.set_runtime_for_tests(None)
+
+
+def test_drift_exchange_matches_mix_derived(tmp_path):
+    """Exchanged control variates (async multi-rank mode, fl/drift.py) and the mix-derived form
+    are the same SCAFFOLD option II under exact same-round mixing on a complete graph: one rank
+    hosting 4 label-shard clients, fp32 wire, forced both ways."""
+    import torch
+    a = _one_rank_run(tmp_path, "mix", drift_exchange="off")
+    b = _one_rank_run(tmp_path, "exch", drift_exchange="on")
+    assert not a.drift.exchange and b.drift.exchange
+    for c in range(4):
+        torch.testing.assert_close(b.client_master[c], a.client_master[c], atol=2e-5, rtol=0)
+        torch.testing.assert_close(b.drift.buf[c], a.drift.buf[c], atol=2e-3, rtol=1e-3)
+
+
+def test_delta_exchange_matches_state_mixing(tmp_path):
+    """Delta exchange (cumulative own updates applied once: the async multi-rank payload) gives
+    the reference's mean of the trained models whenever every update is fresh — here one rank
+    hosting every client, forced both ways."""
+    import torch
+    a = _one_rank_run(tmp_path, "state", gossip_exchange="state")
+    b = _one_rank_run(tmp_path, "delta", gossip_exchange="delta")
+    assert a.gossip.exchange == "state" and b.gossip.exchange == "delta"
+    for c in range(4):
+        torch.testing.assert_close(b.client_master[c], a.client_master[c], atol=2e-5, rtol=0)
