@@ -41,9 +41,12 @@ class FLConfig:
                                         # loss do not depend on it; local eval keeps batch_size
                                         # for the reference's sum-of-batch-means loss quirk)
     global_eval_models: str = "all"     # serverless: "all" = every client model is scored on a
-                                        # disjoint 1/num_clients stride of the global draw (the
-                                        # federation's accuracy; total eval work independent of the
-                                        # GPU count); "client0" = each rank's first client scores
+                                        # disjoint 1/num_clients stride of the global draw (MEAN
+                                        # CLIENT ACCURACY of the federation; total eval work
+                                        # independent of the GPU count); "average" = the mean of
+                                        # the rank's hosted client models on the whole draw (the
+                                        # reference's global_model, serverless_NonIID_IMDB.py:
+                                        # 296-304); "client0" = each rank's first client model on
                                         # the whole draw
     dirichlet_alpha: float = 0.5
     resample_each_round: bool = False   # reference IID scripts draw a fresh random sample every round
@@ -176,7 +179,7 @@ class FLConfig:
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
                    "fedavg_weighting": ("examples", "batches", "uniform"),
-                   "global_eval_models": ("all", "client0")}
+                   "global_eval_models": ("all", "client0", "average")}
         for k, allowed in choices.items():
             if getattr(self, k) not in allowed:
                 raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")

@@ -386,12 +386,18 @@ class Federation:
         if g is not None and hasattr(g, "mark_start"):
             g.mark_start(c, master)
 
-    def _mid_round_targets(self, c: int) -> List[torch.Tensor]:
-        """Buffers that follow a hosted client's model when a neighbour's update is applied
-        mid-round: the drift correction's round-start copy while the client trains."""
-        if self.drift.exchange and self._phase.get(c) == "training":
-            return [self.drift.cv[c]]
-        return []
+    def _mid_round_targets(self, c: int) -> List[tuple]:
+        """Buffers that follow a hosted client when a neighbour's snapshot is applied mid-round:
+        (model space) the drift correction's round-start copy while the client trains, and (aux
+        space) its correction d_c = c_hat - c_c, into which the neighbour's NEW control variate
+        enters at once (the AdamW steps that follow already use it)."""
+        out = []
+        if self.drift.exchange:
+            if self._phase.get(c) == "training":
+                out.append((self.drift.cv[c], "model"))
+            if self.drift.ready.get(c):
+                out.append((self.drift.buf[c], "aux"))
+        return out
 
     def _gossip_poll(self) -> None:
         """Between local steps: let arrived neighbour updates in (non-blocking)."""
@@ -727,11 +733,39 @@ class Federation:
         ``self.flat``: the global model in server mode, the first hosted client in serverless)."""
         if self._sharded_eval():
             return [(c, self.global_test_batches(r, c)) for c in self.local_clients]
+        if self._average_eval():
+            self._refresh_average()
+            return [(-1, self.global_test_batches(r))]
         return [(None, self.global_test_batches(r))]
 
+    def _average_eval(self) -> bool:
+        c = self.cfg
+        return (c.mode == "serverless" and c.global_eval_models == "average" and self.multi
+                and not c.compat_chain)
+
+    @torch.no_grad()
+    def _refresh_average(self) -> None:
+        """Reference-faithful global model (``serverless_NonIID_IMDB.py:296-304``: ONE averaged
+        ``global_model`` scored on the whole draw): the unweighted mean of this rank's hosted
+        client models (every client on one GPU: all of them), cast to the compute dtype."""
+        cs = self.local_clients
+        if not hasattr(self, "_avg_master"):
+            self._avg_master = torch.empty_like(self.flat.master)
+            self._avg_param = torch.empty(self.flat.numel, dtype=self.flat.dtype, device=self.device)
+        src = [self.client_master[c] for c in cs]
+        self._avg_master.copy_(src[0])
+        ops.gossip_mix_(self._avg_master, src[1:], 1.0 / len(src), [1.0 / len(src)] * (len(src) - 1),
+                        self._avg_param if self._avg_param.dtype != torch.float32 else None)
+        if self._avg_param.dtype == torch.float32:
+            self._avg_param.copy_(self._avg_master)
+
     def _bind_client(self, c: Optional[int]) -> None:
-        """Point ``self.flat`` (lane 0's replica) at client c's current state for evaluation."""
+        """Point ``self.flat`` (lane 0's replica) at client c's current state for evaluation
+        (c = -1: the averaged model of ``global_eval_models='average'``)."""
         if c is None or not self.multi:
+            return
+        if c == -1:
+            self.flat.rebind(self._avg_master, self._avg_param)
             return
         if self.lanes:
             self.flat.rebind(self.client_master[c], self.client_param[c])
@@ -739,6 +773,8 @@ class Federation:
             self.flat.load_master(self.client_master[c])
 
     def _client_param(self, c: Optional[int]) -> torch.Tensor:
+        if c == -1:
+            return self._avg_param
         if c is not None and self.lanes:
             return self.client_param[c]
         if c is not None and self.multi:
@@ -960,7 +996,7 @@ class Federation:
                 if gb:
                     self._bind_client(c)
                     acc += self.trainer.evaluate_device(gb)
-            if len(sets) > 1:
+            if len(sets) > 1 or (sets and sets[0][0] == -1):
                 self._bind_client(self.local_clients[0])  # self.flat shows the first client again
             if not self.collective_free:
                 D.all_reduce_(acc)

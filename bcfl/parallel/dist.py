@@ -69,10 +69,32 @@ def init_runtime(device: str = "auto", backend: str = "auto", timeout_s: int = 6
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev
+            kw["pg_options"] = _rccl_options()
         dist.init_process_group(**kw)
         here = True
     _RT = Runtime(rank, world, local_rank, dev, backend, here)
     return _RT
+
+
+def _rccl_options():
+    """Communicator options of the engine's RCCL process group:
+
+    * the collectives run on a HIGH-PRIORITY stream: FedAvg / gossip transfers are issued while
+      the next local step's kernels fill the CUs, and a low-priority communicator stream would
+      queue behind them instead of overlapping;
+    * channels: RCCL's own choice for MI355X unless ``BCFL_RCCL_CHANNELS`` pins both bounds
+      (``NCCL_MIN_NCHANNELS`` / ``NCCL_MAX_NCHANNELS``: more channels spread one collective
+      over more of the 7 xGMI links and more CUs)."""
+    ch = os.environ.get("BCFL_RCCL_CHANNELS")
+    if ch:
+        os.environ.setdefault("NCCL_MIN_NCHANNELS", ch)
+        os.environ.setdefault("NCCL_MAX_NCHANNELS", ch)
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except (AttributeError, RuntimeError):
+        return None
 
 
 def runtime() -> Runtime:
@@ -121,17 +143,34 @@ def all_reduce_bf16_(x: torch.Tensor) -> int:
     rt = runtime()
     if not rt.distributed:
         return 0
+    from .. import ops
     W, n = rt.world, x.numel()
     per = -(-n // W)
-    send = torch.zeros(W * per, dtype=torch.bfloat16, device=x.device)
-    send[:n].copy_(x.reshape(-1))
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send)
-    part = recv.view(W, per).float().sum(0).to(torch.bfloat16)
-    out = torch.empty_like(send)
-    dist.all_gather_into_tensor(out, part)
-    x.reshape(-1).copy_(out[:n])
+    per = -(-per // 64) * 64                  # 128-byte aligned chunks for the vector kernels
+    key = (W * per, x.device)
+    bufs = _BF16_BUFS.get(key)
+    if bufs is None:                          # persistent wire buffers (no per-call allocation)
+        bufs = {"send": torch.zeros(W * per, dtype=torch.bfloat16, device=x.device),
+                "recv": torch.empty(W * per, dtype=torch.bfloat16, device=x.device),
+                "out": torch.empty(W * per, dtype=torch.bfloat16, device=x.device),
+                "acc": torch.empty(per, dtype=torch.float32, device=x.device)}
+        _BF16_BUFS.clear()
+        _BF16_BUFS[key] = bufs
+    send, recv, out, acc = bufs["send"], bufs["recv"], bufs["out"], bufs["acc"]
+    ops.cast_copy_(send[:n], x.reshape(-1))
+    dist.all_to_all_single(recv, send)        # every rank gets all ranks' copy of ITS chunk
+    chunks = list(recv.view(W, per))
+    acc.copy_(chunks[0])
+    # fp32 sum of the W bf16 copies, written back as bf16 into this rank's slot of `out` (one
+    # kernel), then the all-gather of the bf16 chunk sums
+    mine = out.view(W, per)[rt.rank]
+    ops.gossip_mix_(acc, chunks[1:], 1.0, [1.0] * (W - 1), mine)
+    dist.all_gather_into_tensor(out, mine)
+    ops.cast_copy_(x.reshape(-1), out[:n])
     return 2 * (W - 1) * per * 2
+
+
+_BF16_BUFS: dict = {}
 
 
 def broadcast_(t: torch.Tensor, src: int = 0):

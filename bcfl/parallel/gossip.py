@@ -549,11 +549,13 @@ class MailboxGossip:
         n, W = self.numel, self.W_mid
         cuda = self.transport.is_cuda
         for c in self.local:
-            views, ws = [], []
+            views, ws, aviews = [], [], []
             for j in good:
                 if W[c, j] != 0.0:
                     views += [self.stage[j][:n], self.replica[j][:n]]
                     ws += [float(W[c, j]), -float(W[c, j])]
+                    if self.aux is not None:
+                        aviews += [self.stage[j][n:], self.replica[j][n:]]
             if not views:
                 continue
             st = (streams or {}).get(c) if cuda else None
@@ -564,8 +566,13 @@ class MailboxGossip:
                 ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
                 if c in self._started:
                     ops.gossip_mix_(self.start[c], views, 1.0, ws)
-                for t in (also(c) if also is not None else []):
-                    ops.gossip_mix_(t, views, 1.0, ws)
+                for t, half in (also(c) if also is not None else []):
+                    if half == "aux" and aviews:
+                        # aux-space target (drift d_c = c_hat - c_c): the neighbour's new control
+                        # variate replaces its old one in c_hat right away
+                        ops.gossip_mix_(t, aviews, 1.0, ws)
+                    elif half == "model":
+                        ops.gossip_mix_(t, views, 1.0, ws)
                 if cuda:
                     ev = torch.cuda.Event()
                     ev.record(cur)

@@ -222,7 +222,8 @@ def _bf16_ar_worker(rank, world):
     D.init_runtime("cpu", "gloo")
     x = torch.linspace(-1, 1, 1001) * (rank + 1)
     nbytes = D.all_reduce_bf16_(x)
-    assert nbytes == 2 * (world - 1) * 334 * 2
+    per = -(-(-(-1001 // world)) // 64) * 64   # 1/world chunk, padded to 128-byte multiples
+    assert nbytes == 2 * (world - 1) * per * 2
     return x
 
 
@@ -355,3 +356,24 @@ def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path):
     assert torch.equal(r0["G"], r1["G"])               # same live set again -> same G
     for r in res:
         assert int(r["audit_checked"]) > 0 and int(r["audit_mismatched"]) == 0
+
+
+@pytest.mark.slow
+def test_server_world8_allreduce_equals_mailbox_fedavg(tmp_path):
+    """on 8 ranks (one client each, the 8-GPU layout) server FedAvg through the
+    collective all-reduce, through the bf16-delta all-to-all + all-gather wire and through the
+    one-sided mailbox FedAvg reach the same global model (fp32 paths: summation order only;
+    bf16 wire: within the rounding of one round's update)."""
+    kw = {"num_clients": 8, "num_rounds": 2, "train_samples": 32, "test_samples": 16,
+          "global_test_samples": 32}
+    a = run_world(_fed_worker, 8, str(tmp_path / "a"), "server", str(tmp_path / "a"), kw)
+    b = run_world(_fed_worker, 8, str(tmp_path / "b"), "server", str(tmp_path / "b"),
+                  {**kw, "server_transport": "mailbox"})
+    c = run_world(_fed_worker, 8, str(tmp_path / "c"), "server", str(tmp_path / "c"),
+                  {**kw, "server_wire_dtype": "bf16"})
+    for r in range(8):
+        assert torch.equal(a[r]["master"], a[0]["master"])
+        assert torch.equal(b[r]["master"], b[0]["master"])
+        assert torch.equal(c[r]["master"], c[0]["master"])
+    torch.testing.assert_close(b[0]["master"], a[0]["master"], atol=1e-6, rtol=0)
+    torch.testing.assert_close(c[0]["master"], a[0]["master"], atol=2e-4, rtol=0)

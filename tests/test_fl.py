@@ -428,3 +428,16 @@ def test_delta_exchange_matches_state_mixing(tmp_path):
     assert a.gossip.exchange == "state" and b.gossip.exchange == "delta"
     for c in range(4):
         torch.testing.assert_close(b.client_master[c], a.client_master[c], atol=2e-5, rtol=0)
+
+
+def test_global_eval_average_model_is_reference_global_model(tmp_path):
+    """global_eval_models='average' scores ONE model, the unweighted mean of the client models,
+    on the whole draw — the reference serverless global_model (serverless_NonIID_IMDB.py:296-304)
+    — while the default 'all' reports the mean client accuracy on disjoint strides."""
+    import torch
+    fed = _one_rank_run(tmp_path, "avg", global_eval_models="average", topology="ring",
+                        gossip_exchange="state")
+    mean = torch.stack([fed.client_master[c] for c in range(4)]).mean(0)
+    torch.testing.assert_close(fed._avg_master, mean, atol=1e-6, rtol=0)
+    h = fed.history[-1]
+    assert h["global_eval_rows"] == 40 and 0.0 <= h["global_acc"] <= 1.0

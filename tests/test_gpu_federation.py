@@ -34,29 +34,21 @@ def _run(tmp, lanes, overlap):
     return out
 
 
-_K9 = pytest.mark.xfail(reason="with the K9 split-M weight-gradient kernel pinned, lane runs "
-                        "differ from one lane by <= 1.2e-7 in the embedding tables and overlap runs "
-                        "by ~1e-5 (scripts/lanes_diag2.py, profiles/lanes_bitwise_diag_r3.txt); the 8-phase kernel "
-                        "(the default) is bitwise in every configuration", strict=False)
-
-
-@pytest.mark.parametrize("wgrad_kernel", [pytest.param("0", marks=_K9), "1"])  # K9 / gemm8, BOTH runs
 @pytest.mark.parametrize("lanes,overlap", [(3, False), (3, True), (1, True)])
-def test_gpu_lanes_match_sequential(tmp_path, monkeypatch, lanes, overlap, wgrad_kernel):
-    """Every BERT GEMM, the attention and the reductions are bcfl's own kernels, so concurrent
-    lanes and side-stream weight gradients reproduce one-lane training: bit for bit in most runs
-    (then the ledger's update roots agree too), within a few fp32 ULPs of the masters in the rest
-    (the round-3 suite saw one 5.2e-8 difference with 3 lanes: a timing-dependent summation order
-    is left somewhere, under investigation). The weight-gradient kernel is pinned for both runs."""
-    monkeypatch.setenv("BCFL_WGRAD_G8", wgrad_kernel)
+def test_gpu_lanes_match_sequential(tmp_path, lanes, overlap):
+    """Every BERT GEMM (the 8-phase gemm8 kernels, including the weight gradients), the
+    attention and the reductions are bcfl's own deterministic kernels, so concurrent lanes and
+    side-stream weight gradients reproduce one-lane training BIT FOR BIT: masters, loss curve
+    and the ledger's update roots. (The K9 weight-gradient kernel of gemm.hip only serves shapes
+    that are not 256-multiples — ALBERT's 128-wide embedding projection — and is pinned by
+    tests/test_gpu_kernels.py::test_wgrad_split_m.)"""
     a = _run(str(tmp_path / "ref"), 1, False)
     b = _run(str(tmp_path / "x"), lanes, overlap)
     assert torch.isfinite(a[0]).all()
     d = (a[0] - b[0]).abs().max().item()
-    assert d <= 1e-6, d
-    assert a[1] == pytest.approx(b[1], rel=1e-5)
-    if d == 0.0:
-        assert a[2] == b[2]
+    assert torch.equal(a[0], b[0]), f"lane run differs from one lane by {d:.3e}"
+    assert a[1] == b[1]
+    assert a[2] == b[2]
 
 
 def test_gpu_lanes_close_to_sequential(tmp_path):
