@@ -766,6 +766,43 @@ Tensor lora_dgrad(Tensor g_, Tensor w, Tensor gb, Tensor a) {
   return out;
 }
 
+// Tall-skinny LoRA products (skinny.hip): out[M, Cz] = scale * X[M, K] W[R, K]^T (columns
+// R..Cz-1 zero: the padded tail operand of lora_fwd / lora_dgrad) and out[R, N] = scale *
+// P[M, R]^T X[M, N]; both HBM-bound single passes over X with split fp32 partials
+Tensor skinny_xwt(Tensor x, Tensor w, int64_t cz, double scale) {
+  check_gemm_operand(x, "x");
+  check_gemm_operand(w, "w");
+  TORCH_CHECK(x.size(1) == w.size(1) && w.size(0) <= 64 && cz >= w.size(0) && cz % 8 == 0,
+              "skinny_xwt: x [M,K], w [R<=64,K], cz >= R");
+  const int M = x.size(0), K = x.size(1), R = w.size(0);
+  int kc = 0;
+  const int S = bcfl::skinny_xwt_splits(M, K, &kc);
+  const int RP = (R + 15) / 16 * 16;
+  auto part = torch::empty({S, M, RP}, x.options().dtype(torch::kFloat));
+  auto out = torch::empty({M, cz}, x.options());
+  bcfl::SkinnyParams p{x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, 0, K, R, S, kc,
+                       part.data_ptr<float>(), out.data_ptr(), cz, (int)cz, (float)scale};
+  check_rc(bcfl::launch_skinny_xwt(p, stream()), "skinny_xwt");
+  return out;
+}
+
+Tensor skinny_ptx(Tensor pm, Tensor x, double scale) {
+  check_gemm_operand(pm, "p");
+  check_gemm_operand(x, "x");
+  TORCH_CHECK(pm.size(0) == x.size(0) && pm.size(1) <= 64 && pm.size(1) % 8 == 0 && x.size(1) % 64 == 0,
+              "skinny_ptx: p [M,R<=64, R%8==0], x [M,N%64==0]");
+  const int M = x.size(0), N = x.size(1), R = pm.size(1);
+  int mc = 0;
+  const int S = bcfl::skinny_ptx_splits(M, N, &mc);
+  const int RP = (R + 15) / 16 * 16;
+  auto part = torch::empty({S, RP, N}, x.options().dtype(torch::kFloat));
+  auto out = torch::empty({R, N}, x.options());
+  bcfl::SkinnyParams p{x.data_ptr(), x.stride(0), pm.data_ptr(), pm.stride(0), M, N, 0, R, S, mc,
+                       part.data_ptr<float>(), out.data_ptr(), N, 0, (float)scale};
+  check_rc(bcfl::launch_skinny_ptx(p, stream()), "skinny_ptx");
+  return out;
+}
+
 // whether lora_fwd (nn = false: M, N outputs, K) / lora_dgrad (nn = true) take a shape
 bool lora_native_ok(int64_t M, int64_t N, int64_t K, bool nn) {
   bcfl::G8Params g{nullptr, nullptr, nullptr, 8, 8, 8, (int)M, (int)N, (int)K};
@@ -942,6 +979,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw", &adamw);
   m.def("adamw_mt", &adamw_mt);
   m.def("grad_clip_coef", &grad_clip_coef);
+  m.def("skinny_xwt", &skinny_xwt);
+  m.def("skinny_ptx", &skinny_ptx);
   m.def("mix", &mix);
   m.def("axpby", &axpby);
   m.def("cast_copy", &cast_copy);

@@ -112,6 +112,25 @@ int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override = 0);  // s
 void set_g8_persistent(bool on);  // persistent BM=128 g8 grids (BCFL_G8_PERSIST overrides)
 int launch_wgrad_g8(const WgradParams& p, hipStream_t s);
 
+// ---- skinny.hip: tall-skinny LoRA products (HBM-bound) ---------------------------------------
+struct SkinnyParams {
+  const void* X;   // the big operand [M, K] (xwt) / [M, N] (ptx), bf16, row stride ldx
+  int64_t ldx;
+  const void* W;   // the skinny operand: [R, K] (xwt) / [M, R] (ptx), bf16, row stride ldw
+  int64_t ldw;
+  int M, N, K, R;  // R <= 64
+  int S, kc;       // slices and reduction elements per slice (from skinny_*_splits)
+  float* part;     // fp32 [S, M, 16 ceil(R/16)] (xwt) / [S, 16 ceil(R/16), N] (ptx)
+  void* out;       // bf16 [M, Cz] (xwt, columns >= R zero) / [R, N] (ptx), row stride ldo
+  int64_t ldo;
+  int Cz;
+  float scale;
+};
+int skinny_xwt_splits(int M, int K, int* kc);
+int launch_skinny_xwt(const SkinnyParams& p, hipStream_t s);   // out = scale X W^T (+ zero cols)
+int skinny_ptx_splits(int M, int N, int* mc);
+int launch_skinny_ptx(const SkinnyParams& p, hipStream_t s);   // out = scale W^T X
+
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
 enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3, EPI_ACCUM = 4,
                  EPI_PARTIAL = 5 };

@@ -807,6 +807,94 @@ __global__ __launch_bounds__(LN_THREADS) void emb_ln_bwd_kernel(
 }
 
 // ----------------------------------------- RMSNorm -------------------------------------------------
+// Wide-row forms (bf16, H % 512 == 0: Llama's 4096): one row per wave, 16-byte lanes (the 1 KiB
+// wave instruction), the row kept in registers as packed bf16 (4 VGPRs per 8 values) so NC8 = 8
+// chunks cost 32 VGPRs per operand — the 4-wide float forms below hold 64 fp32 values per operand
+// and, for the backward with a frozen weight, a 64 KiB LDS array they never use (2 workgroups
+// per CU): 292 us for [8192, 4096] (profiles/config5_kernel_stats_r3.md) against ~40 us of HBM
+// traffic.
+__device__ __forceinline__ void unpack8(const uint4& u, float f[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <int NC8>
+__global__ __launch_bounds__(LN_THREADS) void rmsnorm_fwd_wide_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+    float* __restrict__ rstd_out, int T, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  uint4 xv[NC8];
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) xv[i] = *reinterpret_cast<const uint4*>(x + base + (lane + i * WAVE) * 8);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    float f[8];
+    unpack8(xv[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss += f[k] * f[k];
+  }
+  const float r = rsqrtf(wave_sum(ss) / H + eps);
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    const int col = (lane + i * WAVE) * 8;
+    float f[8], g[8], o[8];
+    unpack8(xv[i], f);
+    unpack8(*reinterpret_cast<const uint4*>(w + col), g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = f[k] * r * g[k];
+    Vec8<bf16_t>::store(out + base + col, o);
+  }
+  if (lane == 0) rstd_out[row] = r;
+}
+
+// dx = r (d . w) - x r^3 mean(d . w . x), frozen weight (no weight gradient)
+template <int NC8>
+__global__ __launch_bounds__(LN_THREADS) void rmsnorm_bwd_wide_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd_in, bf16_t* __restrict__ dx, int T, int H) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  uint4 dv[NC8], xv[NC8];
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    dv[i] = *reinterpret_cast<const uint4*>(dout + base + (lane + i * WAVE) * 8);
+    xv[i] = *reinterpret_cast<const uint4*>(x + base + (lane + i * WAVE) * 8);
+  }
+  const float r = rstd_in[row];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    float d[8], f[8], g[8];
+    unpack8(dv[i], d);
+    unpack8(xv[i], f);
+    unpack8(*reinterpret_cast<const uint4*>(w + (lane + i * WAVE) * 8), g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += d[k] * g[k] * f[k];
+  }
+  const float c = r * r * r * wave_sum(s) / H;
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    const int col = (lane + i * WAVE) * 8;
+    float d[8], f[8], g[8], o[8];
+    unpack8(dv[i], d);
+    unpack8(xv[i], f);
+    unpack8(*reinterpret_cast<const uint4*>(w + col), g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = r * d[k] * g[k] - f[k] * c;
+    Vec8<bf16_t>::store(dx + base + col, o);
+  }
+}
+
 template <typename TA, typename TP, int NCH>
 __global__ __launch_bounds__(LN_THREADS) void rmsnorm_fwd_kernel(
     const TA* __restrict__ x, const TP* __restrict__ w, TA* __restrict__ out,
@@ -1080,6 +1168,14 @@ int launch_rmsnorm_fwd(const void* x, const void* w, void* out, float* rstd, int
                        float eps, int dt, hipStream_t s) {
   if (H % 4) return -2;
   dim3 grid((T + LN_WAVES - 1) / LN_WAVES);
+  if (dt == DT_BF16 && H % 512 == 0 && H <= 8192) {
+    switch (H / 512) {
+#define RMS_W(N) case N: hipLaunchKernelGGL(rmsnorm_fwd_wide_kernel<N>, grid, dim3(LN_THREADS), 0, s, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)out, rstd, T, H, eps); return 0;
+      RMS_W(1) RMS_W(2) RMS_W(4) RMS_W(8) RMS_W(16)
+#undef RMS_W
+      default: break;
+    }
+  }
   DT_DISPATCH(dt, NCH_DISPATCH(H, hipLaunchKernelGGL((rmsnorm_fwd_kernel<TA, TP, NC>), grid,
       dim3(LN_THREADS), 0, s, (const TA*)x, (const TP*)w, (TA*)out, rstd, T, H, eps)));
   return 0;
@@ -1088,6 +1184,15 @@ int launch_rmsnorm_fwd(const void* x, const void* w, void* out, float* rstd, int
 int launch_rmsnorm_bwd(const void* dout, const void* x, const void* w, const float* rstd, void* dx,
                        float* partial, int nblk, int T, int H, int dt, hipStream_t s) {
   if (H % 4) return -2;
+  if (!partial && dt == DT_BF16 && H % 512 == 0 && H <= 8192) {
+    const dim3 grid((T + LN_WAVES - 1) / LN_WAVES);
+    switch (H / 512) {
+#define RMS_W(N) case N: hipLaunchKernelGGL(rmsnorm_bwd_wide_kernel<N>, grid, dim3(LN_THREADS), 0, s, (const bf16_t*)dout, (const bf16_t*)x, (const bf16_t*)w, rstd, (bf16_t*)dx, T, H); return 0;
+      RMS_W(1) RMS_W(2) RMS_W(4) RMS_W(8) RMS_W(16)
+#undef RMS_W
+      default: break;
+    }
+  }
   DT_DISPATCH(dt, NCH_DISPATCH(H, hipLaunchKernelGGL((rmsnorm_bwd_kernel<TA, TP, NC>), dim3(nblk),
       dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)x, (const TP*)w, rstd, (TA*)dx, partial,
       T, H)));

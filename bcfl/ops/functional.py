@@ -20,7 +20,7 @@ import torch
 
 from . import ref
 from . import rng as _rng
-from ._native import native, use_native
+from ._native import available as native_available, native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
@@ -319,6 +319,14 @@ _EPI_PARTIAL = 5  # gemm8.hip fp32 split-K partials
 # (profiles/lora_tail_r3.json)
 _LORA_G8_SKINNY = os.environ.get("BCFL_LORA_G8", "0") == "1"
 _LORA_PAD = 256   # the low-rank dimension padded to one 8-phase GEMM column tile
+# the four tall-skinny low-rank products on skinny.hip (HBM-bound single passes over x / g);
+# BCFL_LORA_SKINNY=0: the library GEMMs (A/B)
+_LORA_SKINNY = os.environ.get("BCFL_LORA_SKINNY", "1") == "1"
+
+
+def _skinny_ok(nr: int, M: int, N: int, K: int) -> bool:
+    return (_LORA_SKINNY and nr <= 64 and nr % 8 == 0 and K % 64 == 0 and N % 64 == 0
+            and native_available())
 
 
 def _g8_skinny(A: torch.Tensor, B: torch.Tensor, b_col: bool, ways: int = 4) -> torch.Tensor:
@@ -364,7 +372,15 @@ class _LoRALinear(torch.autograd.Function):
                  and N % 256 == 0 and K % 256 == 0
                  and _lora_tail_ok(M, N, K, False, x2, w) and _lora_tail_ok(M, K, N, True, x2, w))
         ctx.fused = fused
-        if fused:
+        ctx.skinny = fused and _skinny_ok(nr, M, N, K)
+        if ctx.skinny:
+            k2 = _lora_k2(nr)
+            xa_f = native().skinny_xwt(x2, a, k2, 1.0)      # [M, k2], columns >= n r zero
+            bb_p = w.new_zeros(N, k2)
+            torch.mul(bbd, s, out=bb_p[:, :nr])
+            y = native().lora_fwd(x2, w, xa_f, bb_p)
+            ctx.save_for_backward(x2, w, a, xa_f, bb_p)
+        elif fused:
             k2 = _lora_k2(nr)
             if _LORA_G8_SKINNY:
                 a_p = a.new_zeros(_LORA_PAD, K)
@@ -396,6 +412,24 @@ class _LoRALinear(torch.autograd.Function):
             g2 = g2.contiguous()
         dx = da = None
         dbs = [None] * len(sizes)
+        if ctx.skinny:
+            x2, w, a, xa_f, bb_p = ctx.saved_tensors
+            nr, k2 = a.shape[0], xa_f.shape[1]
+            C = native()
+            # gbs = g (s Bbd) [M, k2] (zero past n r): the dgrad tail operand and dA's left factor
+            gbs = C.skinny_xwt(g2, bb_p[:, :nr].t().contiguous(), k2, 1.0)
+            if ctx.needs_input_grad[0]:
+                dx = C.lora_dgrad(g2, w, gbs, a).view(ctx.xshape)
+            if ctx.needs_input_grad[2]:
+                da = C.skinny_ptx(gbs[:, :nr], x2, 1.0)           # (s g Bbd)^T x  [n r, K]
+            if any(ctx.needs_input_grad[5:]):
+                full_t = C.skinny_ptx(xa_f[:, :nr], g2, s)        # s xa^T g  [n r, N]
+                r = nr // len(sizes)
+                o = 0
+                for i, n in enumerate(sizes):
+                    dbs[i] = full_t[i * r:(i + 1) * r, o:o + n].t().contiguous()
+                    o += n
+            return (dx, None, da, None, None, *dbs)
         if ctx.fused:
             x2, w, a, xa_f, bb_p = ctx.saved_tensors
             nr = a.shape[0]

@@ -745,3 +745,50 @@ def test_grad_clip_coef_and_clipped_adamw(with_g2):
                    0.999, 1e-6, 0.0, "hf")
     _close(m, rmm, 1e-6, 1e-5)
     _close(master, rm, 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("M,K,R,cz", [(8192, 4096, 48, 128), (8000, 4096, 16, 128),
+                                      (777, 1024, 32, 32), (8192, 14336, 32, 128)])
+def test_skinny_xwt_matches_fp32(M, K, R, cz):
+    """LoRA tall-skinny product out = scale * X W^T (skinny.hip), zero columns past R."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(R, K, device=DEV) * K ** -0.5).bfloat16()
+    out = ops.native().skinny_xwt(x, w, cz, 2.0)
+    ref_ = 2.0 * (x.float() @ w.float().t())
+    assert out.shape == (M, cz)
+    _close(out[:, :R], ref_, 2e-2, 2e-2)
+    assert (out[:, R:] == 0).all()
+    assert torch.equal(out, ops.native().skinny_xwt(x, w, cz, 2.0))   # deterministic slices
+
+
+@pytest.mark.parametrize("M,N,R", [(8192, 4096, 48), (8000, 6144, 16), (640, 1024, 32),
+                                   (8192, 28672, 32)])
+def test_skinny_ptx_matches_fp32(M, N, R):
+    """LoRA adapter-gradient product out = scale * P^T X over the M tokens (skinny.hip: both
+    operands through LDS, hardware-transposed reads)."""
+    torch.manual_seed(1)
+    p = torch.randn(M, R, device=DEV).bfloat16()
+    x = torch.randn(M, N, device=DEV).bfloat16()
+    out = ops.native().skinny_ptx(p, x, 0.5)
+    ref_ = 0.5 * (p.float().t() @ x.float())
+    assert out.shape == (R, N)
+    _close(out, ref_, 2e-2, 2e-2)
+    assert torch.equal(out, ops.native().skinny_ptx(p, x, 0.5))
+
+
+@pytest.mark.parametrize("T,H", [(1000, 4096), (65, 1024)])
+def test_rmsnorm_wide_rows_frozen_weight(T, H):
+    """Wide-row RMSNorm (Llama H = 4096, packed-bf16 rows, 16-byte lanes) with a FROZEN weight
+    (LoRA: no weight gradient) vs the fp32 reference, forward and input gradient."""
+    torch.manual_seed(3)
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    out = ops.rmsnorm(x, w, 1e-5)
+    xf = x.detach().float().requires_grad_(True)
+    r = ref.rmsnorm(xf, w.float(), 1e-5)
+    _close(out, r, 3e-2)
+    go = torch.randn_like(out)
+    out.backward(go)
+    r.backward(go.float())
+    _grads_close([x.grad], [xf.grad])
