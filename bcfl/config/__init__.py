@@ -69,6 +69,9 @@ class FLConfig:
                                         # partitions (label_shards, ref_contiguous, dirichlet),
                                         # none for IID ones
     drift_correction_scale: float = 1.0
+    outer_lr: float = 1.0               # round-level outer optimizer on the pseudo-gradient
+    outer_momentum: float = 0.0         # x_prev - x_agg (fl/outer.py): lr 1 + momentum 0 = the
+    outer_nesterov: bool = True         # reference's plain average; momentum > 0 = FedAvgM
     dropout: Optional[float] = None     # None -> model default
     dtype: str = "bf16"                 # compute dtype on GPU ("bf16" | "fp32")
     # --- federation ------------------------------------------------------------

@@ -727,13 +727,20 @@ void linear_fwd_acc(Tensor x, Tensor w, Tensor into) {
 //               (xa = x A^T and bb = s Bbd, both zero-padded to K2 = 128 columns)
 //   lora_dgrad: dx[M, K] = g[M, N] w[N, K] + gb[M, K2] a[r2, K]
 //               (gb = s g Bbd zero-padded to K2 columns; a = the stacked A, r2 <= K2 valid rows)
-Tensor lora_fwd(Tensor x, Tensor w, Tensor xa, Tensor bb) {
+Tensor lora_fwd(Tensor x, Tensor w, Tensor xa, Tensor bb, optional<Tensor> res) {
   for (auto* t : {&x, &w, &xa, &bb}) check_gemm_operand(*t, "lora_fwd operand");
   const int M = x.size(0), N = w.size(0), K = x.size(1), K2 = xa.size(1);
   TORCH_CHECK(w.size(1) == K && xa.size(0) == M && bb.size(0) == N && bb.size(1) == K2,
               "lora_fwd: x [M,K], w [N,K], xa [M,K2], bb [N,K2]");
   auto out = torch::empty({M, N}, x.options());
   bcfl::G8Params g{x.data_ptr(), w.data_ptr(), out.data_ptr(), x.stride(0), w.stride(0), N, M, N, K};
+  if (res.has_value() && res->defined()) {  // + residual in the epilogue (no separate add pass)
+    check_gemm_operand(*res, "lora_fwd residual");
+    TORCH_CHECK(res->size(0) == M && res->size(1) == N, "lora_fwd: residual [M,N]");
+    g.epi = bcfl::EPI_RESID;
+    g.aux = res->data_ptr();
+    g.ldaux = res->stride(0);
+  }
   g.kc = K;
   g.bm = bcfl::g8_auto_bm(M, N, 1);
   g.A2 = xa.data_ptr();
@@ -958,7 +965,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "persistent BM=128 8-phase GEMM grids for launches with more tiles than CUs");
   m.def("linear_dgrad_acc", &linear_dgrad_acc);
   m.def("linear_fwd_acc", &linear_fwd_acc);
-  m.def("lora_fwd", &lora_fwd);
+  m.def("lora_fwd", &lora_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("xa"),
+        pybind11::arg("bb"), pybind11::arg("res") = pybind11::none());
   m.def("lora_dgrad", &lora_dgrad);
   m.def("lora_native_ok", &lora_native_ok);
   m.def("gemm_native_ok", &gemm_native_ok);

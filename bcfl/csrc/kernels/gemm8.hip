@@ -539,6 +539,11 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
                 Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, av);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] *= act_dt<ACT>(av[e]);
+              } else if constexpr (EPI == EPI_RESID) {  // residual stream add (Llama x + o)
+                float rv[8];
+                Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, rv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += rv[e];
               } else if constexpr (EPI == EPI_ACCUM) {
                 float ov[8];
                 Vec8<bf16_t>::load(Cp + (int64_t)m * p.ldc + n, ov);
@@ -641,14 +646,19 @@ int g8_dispatch_t(const G8Params& p, hipStream_t s, int nwg) {
   return 0;
 }
 
-// tail-segment launches (EPI_STORE only: the LoRA base + low-rank products of _LoRALinear)
+// tail-segment launches (the LoRA base + low-rank products of _LoRALinear): EPI_STORE, and
+// EPI_RESID for the forward projections that feed the residual stream (o_proj, down_proj)
 template <int BM, bool BCOL, bool PERSIST>
 int g8_dispatch_tail(const G8Params& p, hipStream_t s, int nwg) {
-  if (p.epi != EPI_STORE) return -4;
   constexpr int SLAB = T8 / 64 * G8<BM, false, BCOL, 0, 0>::QM * (G8<BM, false, BCOL, 0, 0>::QN + 4) * 4;
   constexpr size_t lds = G8<BM, false, BCOL, 0, 0>::LDS + (PERSIST ? SLAB : 0);
   const dim3 grid(PERSIST ? 256 : nwg), block(T8);
-  hipLaunchKernelGGL((g8_kernel<BM, false, BCOL, EPI_STORE, 0, PERSIST, true>), grid, block, lds, s, p);
+  if (p.epi == EPI_STORE)
+    hipLaunchKernelGGL((g8_kernel<BM, false, BCOL, EPI_STORE, 0, PERSIST, true>), grid, block, lds, s, p);
+  else if (p.epi == EPI_RESID && !BCOL)
+    hipLaunchKernelGGL((g8_kernel<BM, false, false, EPI_RESID, 0, PERSIST, true>), grid, block, lds, s, p);
+  else
+    return -4;
   return 0;
 }
 
@@ -753,7 +763,8 @@ int g8_supported(const G8Params& p) {
   if (p.epi == EPI_PARTIAL && !p.part) return -3;
   if (p.K2 > 0) {  // tail segment: one split, ROW A2, K2 a whole number of K-tile pairs
     if (p.a_col || p.splits != 1 || p.K2 % 128 || !p.A2 || !p.B2 || p.lda2 % 8 || p.ldb2 % 8) return -3;
-    if (p.epi != EPI_STORE) return -4;
+    if (p.epi != EPI_STORE && !(p.epi == EPI_RESID && !p.b_col && p.aux && p.ldaux % 8 == 0))
+      return -4;
     if (p.b_col && (p.K2rows <= 0 || p.K2rows > p.K2)) return -3;
   }
   return 0;

@@ -133,7 +133,7 @@ int launch_skinny_ptx(const SkinnyParams& p, hipStream_t s);   // out = scale W^
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
 enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3, EPI_ACCUM = 4,
-                 EPI_PARTIAL = 5 };
+                 EPI_PARTIAL = 5, EPI_RESID = 6 };  // RESID: C = A B (+ tail) + aux (residual)
 struct LinearParams {
   const void* A;       // [M, K] bf16, row stride lda
   const void* B;       // NT: [N, K] (ldb);  NN: [K, N] (ldb)

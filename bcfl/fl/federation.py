@@ -47,6 +47,7 @@ from ..trust.anomaly import UpdateAnomalyFilter, Verdicts
 from ..trust.ledger import Ledger
 from ..utils.obs import MetricsWriter, PhaseTimer, Telemetry
 from .drift import DriftCorrection, resolve_mode as resolve_drift
+from .outer import OuterOptimizer
 from .trainer import EvalResult, LocalTrainer, MicroReplica
 
 DATA_SEED = 1234
@@ -162,6 +163,11 @@ class Federation:
         self.drift = DriftCorrection(resolve_drift(cfg.drift_correction, cfg.partition),
                                      cfg.drift_correction_scale,
                                      self.local_clients, self.flat.numel, self.device)
+        # round-level outer optimizer (FedAvgM / outer Nesterov; default lr 1, momentum 0 = the
+        # reference's plain average): server mode keys the global model as -1
+        self.outer = OuterOptimizer(cfg.outer_lr, cfg.outer_momentum, cfg.outer_nesterov,
+                                    [-1] if cfg.mode == "server" else self.local_clients,
+                                    self.flat.numel, self.device)
         ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else len(self.lanes) <= 1
         if cfg.deterministic:
             ov = False  # the overlapped path's gradients are not bitwise reproducible
@@ -1096,10 +1102,11 @@ class Federation:
             else:
                 D.all_reduce_(self.acc)
                 wire_bytes = self.acc.numel() * 4 * 2 * max(self.rt.world - 1, 0) // max(self.rt.world, 1)
+        for c in self.local_clients:   # SCAFFOLD's c' from the plain FedAvg result
+            self.drift.after_mix(c, self.acc)
+        self.outer.step(-1, self.acc, prev=G)   # FedAvgM / outer Nesterov (off by default)
         G.copy_(self.acc)
         self.flat.load_master(G)
-        for c in self.local_clients:
-            self.drift.after_mix(c, G)
         # Flower evaluate_round: every client evaluates the new global model on its test split
         client_metrics = []
         if cfg.eval_local:
@@ -1194,6 +1201,9 @@ class Federation:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
         need_prev = self.filter is not None or bool(cfg.inject_byzantine)
+        if self.outer.enabled:
+            for c in self.local_clients:
+                self.outer.begin(c, self.client_master[c] if self.multi else self.flat.master)
         if self.lanes:
             o = self._train_lanes(r, need_prev)
             sk, nr, losses, local_eval = o["sk"], o["nr"], o["losses"], o["local_eval"]
@@ -1239,6 +1249,13 @@ class Federation:
         self.prev_verdicts = v
         for c in self.local_clients:
             self.drift.after_mix(c, self.client_master[c] if self.multi else self.flat.master)
+        if self.outer.enabled:
+            for c in self.local_clients:
+                if self.multi:
+                    self.outer.step(c, self.client_master[c], self.client_param.get(c))
+                else:
+                    self.outer.step(c, self.flat.master, self.flat.param
+                                    if self.flat.param is not self.flat.master else None)
         if self.multi:  # evaluate this rank's first client's mixed model
             c0 = self.local_clients[0]
             if self.lanes:
@@ -1421,6 +1438,7 @@ class Federation:
                              for c, o in self.client_opt.items()},
               "prev_rejected": sorted(self.prev_verdicts.rejected),
               "drift": self.drift.state_dict(),
+              "outer": self.outer.state_dict(),
               "tokens_trained": int(self.tokens_trained),
               "ledger_tip": self.ledger.tip if self.ledger else None,
               "ledger_height": len(self.ledger) if self.ledger else 0}
@@ -1578,6 +1596,7 @@ class Federation:
             self.global_master.copy_(st["global_master"])
         self.prev_verdicts = Verdicts(rejected=set(int(x) for x in st.get("prev_rejected", [])))
         self.drift.load_state_dict(st.get("drift"))
+        self.outer.load_state_dict(st.get("outer"))
         self.tokens_trained = int(st.get("tokens_trained", 0))
         if self.gossip is not None and "gossip" in st:
             self.gossip.load_state_dict(st["gossip"])

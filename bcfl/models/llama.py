@@ -67,11 +67,12 @@ class LoRA(nn.Module):
         d = outs[0] if len(outs) == 1 else torch.cat(outs, dim=1)
         return d * self.scale
 
-    def fused(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        """x W^T + this adapter's delta, WITHOUT materialising the delta as a separate pass:
-        the low-rank product writes the output buffer and the base GEMM accumulates into it
-        (ops.lora_linear; GPU). CPU / unsupported: the unfused reference."""
-        return ops.lora_linear(x, w, self.A, list(self.B), self.scale)
+    def fused(self, x: torch.Tensor, w: torch.Tensor,
+              residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x W^T + this adapter's delta (+ ``residual``), WITHOUT materialising the delta or the
+        sum as separate passes: the low-rank product is a tail of the base GEMM's reduction and
+        the residual add its epilogue (ops.lora_linear; GPU). CPU: the unfused reference."""
+        return ops.lora_linear(x, w, self.A, list(self.B), self.scale, residual)
 
 
 class LlamaLayer(nn.Module):
@@ -109,14 +110,17 @@ class LlamaLayer(nn.Module):
             ctx = ops.query_subset_attention(qkv, rows, batch.cu_seqlens, batch.max_seqlen, nh,
                                              nkv, d, 0.0, self.training, causal=True)
             x = x.index_select(0, rows.long())
-        o = self.lora_o.fused(ctx, self.o_weight) if self.lora else ops.linear(ctx, self.o_weight)
-        x = x + o
+        if self.lora:   # residual adds fused into the projections' GEMM epilogues
+            x = self.lora_o.fused(ctx, self.o_weight, residual=x)
+        else:
+            x = x + ops.linear(ctx, self.o_weight)
         h2 = ops.rmsnorm(x, self.post_ln, c.rms_norm_eps)
         gu = (self.lora_gate_up.fused(h2, self.gate_up_weight) if self.lora
               else ops.linear(h2, self.gate_up_weight))
         a = ops.swiglu(gu)
-        dn = self.lora_down.fused(a, self.down_weight) if self.lora else ops.linear(a, self.down_weight)
-        return x + dn
+        if self.lora:
+            return self.lora_down.fused(a, self.down_weight, residual=x)
+        return x + ops.linear(a, self.down_weight)
 
 
 class LlamaForSequenceClassification(SeqClassifierBase):

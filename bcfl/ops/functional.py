@@ -361,7 +361,7 @@ class _LoRALinear(torch.autograd.Function):
     output and the base GEMM accumulates in place."""
 
     @staticmethod
-    def forward(ctx, x, w, a, s, sizes, *bs):
+    def forward(ctx, x, w, a, s, sizes, res, *bs):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.stride(-1) != 1 or x2.stride(0) % 8:
             x2 = x2.contiguous()
@@ -373,12 +373,20 @@ class _LoRALinear(torch.autograd.Function):
                  and _lora_tail_ok(M, N, K, False, x2, w) and _lora_tail_ok(M, K, N, True, x2, w))
         ctx.fused = fused
         ctx.skinny = fused and _skinny_ok(nr, M, N, K)
+        ctx.has_res = res is not None
+        res2 = None
+        if res is not None:
+            res2 = res.reshape(-1, N)
+            if res2.stride(-1) != 1 or res2.stride(0) % 8:
+                res2 = res2.contiguous()
         if ctx.skinny:
             k2 = _lora_k2(nr)
             xa_f = native().skinny_xwt(x2, a, k2, 1.0)      # [M, k2], columns >= n r zero
             bb_p = w.new_zeros(N, k2)
             torch.mul(bbd, s, out=bb_p[:, :nr])
-            y = native().lora_fwd(x2, w, xa_f, bb_p)
+            # the residual stream add rides on the GEMM epilogue (EPI_RESID)
+            y = native().lora_fwd(x2, w, xa_f, bb_p, res2)
+            res2 = None
             ctx.save_for_backward(x2, w, a, xa_f, bb_p)
         elif fused:
             k2 = _lora_k2(nr)
@@ -402,6 +410,8 @@ class _LoRALinear(torch.autograd.Function):
                 y.addmm_(x2, w.t())
             ctx.save_for_backward(x2, w, a, xa, bbd)
         ctx.s, ctx.sizes, ctx.xshape = s, sizes, x.shape
+        if res2 is not None:
+            y = y + res2
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -429,7 +439,7 @@ class _LoRALinear(torch.autograd.Function):
                 for i, n in enumerate(sizes):
                     dbs[i] = full_t[i * r:(i + 1) * r, o:o + n].t().contiguous()
                     o += n
-            return (dx, None, da, None, None, *dbs)
+            return (dx, None, da, None, None, g if ctx.has_res else None, *dbs)
         if ctx.fused:
             x2, w, a, xa_f, bb_p = ctx.saved_tensors
             nr = a.shape[0]
@@ -451,7 +461,7 @@ class _LoRALinear(torch.autograd.Function):
                 for i, n in enumerate(sizes):
                     dbs[i] = full[o:o + n, i * r:(i + 1) * r].contiguous()
                     o += n
-            return (dx, None, da, None, None, *dbs)
+            return (dx, None, da, None, None, g if ctx.has_res else None, *dbs)
         x2, w, a, xa, bbd = ctx.saved_tensors
         gb = g2 @ bbd                                     # [M, n r]
         if ctx.needs_input_grad[0]:
@@ -466,18 +476,22 @@ class _LoRALinear(torch.autograd.Function):
             for i, n in enumerate(sizes):
                 dbs[i] = full[o:o + n, i * r:(i + 1) * r].contiguous()
                 o += n
-        return (dx, None, da, None, None, *dbs)
+        return (dx, None, da, None, None, g if ctx.has_res else None, *dbs)
 
 
-def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, bs, s: float) -> torch.Tensor:
-    """Frozen base projection + LoRA delta, fused on the GPU (see :class:`_LoRALinear`)."""
+def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, bs, s: float,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Frozen base projection + LoRA delta (+ ``residual``), fused on the GPU (see
+    :class:`_LoRALinear`: the residual add rides on the GEMM epilogue)."""
     if use_native(x, "lora") and not w.requires_grad and x.dtype == torch.bfloat16:
-        return _LoRALinear.apply(x, w, a, float(s), tuple(int(b.shape[0]) for b in bs), *bs)
+        return _LoRALinear.apply(x, w, a, float(s), tuple(int(b.shape[0]) for b in bs), residual,
+                                 *bs)
     xa = linear(x, a)
     r = a.shape[0] // len(bs)
     outs = [linear(xa[..., i * r:(i + 1) * r], b) for i, b in enumerate(bs)]
     d = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
-    return linear(x, w) + d * s
+    y = linear(x, w) + d * s
+    return y if residual is None else residual + y
 
 
 def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:

@@ -441,3 +441,25 @@ def test_global_eval_average_model_is_reference_global_model(tmp_path):
     torch.testing.assert_close(fed._avg_master, mean, atol=1e-6, rtol=0)
     h = fed.history[-1]
     assert h["global_eval_rows"] == 40 and 0.0 <= h["global_acc"] <= 1.0
+
+
+def test_outer_optimizer_nesterov_and_heavy_ball():
+    """fl/outer.py: x_new = x_prev - lr (g + mu v) (Nesterov) / x_prev - lr v, v = mu v + g,
+    g = x_prev - x_agg; lr 1 + momentum 0 is disabled (the reference's plain average)."""
+    import torch
+    from bcfl.fl.outer import OuterOptimizer
+    assert not OuterOptimizer(1.0, 0.0, True, [0], 4, "cpu").enabled
+    for nest in (True, False):
+        o = OuterOptimizer(0.7, 0.9, nest, [0], 4, "cpu")
+        v = torch.zeros(4)
+        x = torch.tensor([1.0, 2.0, 3.0, 4.0])
+        for t in range(3):
+            agg = x - 0.1 * (t + 1) * torch.tensor([1.0, -1.0, 0.5, 2.0])
+            g = x - agg
+            v = 0.9 * v + g
+            want = x - 0.7 * ((g + 0.9 * v) if nest else v)
+            o.begin(0, x)
+            got = agg.clone()
+            o.step(0, got)
+            torch.testing.assert_close(got, want, atol=1e-6, rtol=0)
+            x = got

@@ -537,12 +537,14 @@ def test_native_dropout_mask_matches_hash_layout():
     _close(y, r, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("T", [1000, 2048, 4096])
-def test_lora_linear_fused_matches_unfused(T):
+@pytest.mark.parametrize("T,with_res", [(1000, False), (2048, False), (4096, False),
+                                        (4096, True), (1000, True)])
+def test_lora_linear_fused_matches_unfused(T, with_res):
     """ops.lora_linear == the unfused x W^T + cat(xa_i B_i^T) * s path, forward and gradients.
     T = 1000: the two-GEMM path (low-rank product written first, base GEMM accumulating);
     T >= 1024: every product on the 8-phase GEMM (split-K skinny GEMMs, tail segments, weight-
-    gradient kernel)."""
+    gradient kernel; since round 4 the four tall-skinny products on skinny.hip). ``with_res``:
+    + a residual stream input, added in the GEMM epilogue (EPI_RESID) on the fused path."""
     import os
     torch.manual_seed(4)
     K, r = 512, 16
@@ -552,6 +554,7 @@ def test_lora_linear_fused_matches_unfused(T):
     a0 = (torch.randn(len(sizes) * r, K, device=DEV) * 0.05).bfloat16()
     b0 = [(torch.randn(n, r, device=DEV) * 0.05).bfloat16() for n in sizes]
     g = torch.randn(T, sum(sizes), device=DEV).bfloat16()
+    r0 = torch.randn(T, sum(sizes), device=DEV).bfloat16()
     res = {}
     for route in ("bcfl", "torch"):
         os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "lora"
@@ -559,9 +562,10 @@ def test_lora_linear_fused_matches_unfused(T):
             x = x0.clone().requires_grad_(True)
             a = a0.clone().requires_grad_(True)
             bs = [b.clone().requires_grad_(True) for b in b0]
-            y = ops.lora_linear(x, w, a, bs, 2.0)
+            rr = r0.clone().requires_grad_(True) if with_res else None
+            y = ops.lora_linear(x, w, a, bs, 2.0, rr)
             y.backward(g)
-            res[route] = [y, x.grad, a.grad] + [b.grad for b in bs]
+            res[route] = [y, x.grad, a.grad] + [b.grad for b in bs] + ([rr.grad] if with_res else [])
         finally:
             os.environ["BCFL_TORCH_OPS"] = ""
     for u, v in zip(res["bcfl"], res["torch"]):
