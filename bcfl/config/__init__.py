@@ -97,6 +97,10 @@ class FLConfig:
                                         # delta for multi-rank async gossip on complete graphs
     gossip_apply_on_arrival: bool = True  # delta exchange: apply neighbours' updates between
                                           # local steps as they arrive (non-blocking polls)
+    gossip_max_lead: int = 2            # async mailbox gossip: bounded staleness (SSP) — do not
+    #                                     start a round while a live neighbour's newest applied
+    #                                     update is > this many rounds behind (0 = unbounded)
+    gossip_lead_timeout_s: float = 5.0  # ... a neighbour still behind after this counts as dead
     gossip_stale_decay: float = 0.0     # async mailbox mix: a view k rounds behind keeps
                                         # W / (1 + decay * k) of its weight (rest -> self)
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl

@@ -773,6 +773,59 @@ Tensor lora_dgrad(Tensor g_, Tensor w, Tensor gb, Tensor a) {
   return out;
 }
 
+// LoRA MLP with SwiGLU in the GEMM epilogues (config 5's gate|up and down projections):
+//   lora_fwd_swiglu:   gu[M, 2I] = x w^T + xa bb^T (w = [gate; up] [2I, K]), act = silu(gate) * up
+//                      -> {act [M, I], gu}  (no separate SwiGLU pass, gu saved for the backward)
+//   lora_dgrad_swiglu: dA = g w_down + gb a (never stored) -> dgu [M, 2I] = SwiGLU'(gu) . dA
+std::vector<Tensor> lora_fwd_swiglu(Tensor x, Tensor w, Tensor xa, Tensor bb) {
+  for (auto* t : {&x, &w, &xa, &bb}) check_gemm_operand(*t, "lora_fwd_swiglu operand");
+  const int M = x.size(0), N = w.size(0), K = x.size(1), K2 = xa.size(1);
+  TORCH_CHECK(w.size(1) == K && xa.size(0) == M && bb.size(0) == N && bb.size(1) == K2 && N % 256 == 0,
+              "lora_fwd_swiglu: x [M,K], w [2I,K], xa [M,K2], bb [2I,K2], I % 128 == 0");
+  const int I = N / 2;
+  auto act = torch::empty({M, I}, x.options());
+  auto gu = torch::empty({M, N}, x.options());
+  bcfl::G8Params g{x.data_ptr(), w.data_ptr(), act.data_ptr(), x.stride(0), w.stride(0), I, M, N, K};
+  g.epi = bcfl::EPI_SWIGLU;
+  g.aux = gu.data_ptr();
+  g.ldaux = N;
+  g.pair = I;
+  g.kc = K;
+  g.bm = bcfl::g8_auto_bm(M, N, 1);
+  g.A2 = xa.data_ptr();
+  g.B2 = bb.data_ptr();
+  g.lda2 = xa.stride(0);
+  g.ldb2 = bb.stride(0);
+  g.K2 = K2;
+  g.K2rows = K2;
+  check_rc(bcfl::launch_g8(g, stream()), "lora_fwd_swiglu");
+  return {act, gu};
+}
+
+Tensor lora_dgrad_swiglu(Tensor g_, Tensor w, Tensor gb, Tensor a, Tensor gu) {
+  for (auto* t : {&g_, &w, &gb, &a, &gu}) check_gemm_operand(*t, "lora_dgrad_swiglu operand");
+  const int M = g_.size(0), N = w.size(0), I = w.size(1), K2 = gb.size(1), R = a.size(0);
+  TORCH_CHECK(g_.size(1) == N && gb.size(0) == M && a.size(1) == I && R <= K2 && gu.size(0) == M &&
+              gu.size(1) == 2 * I, "lora_dgrad_swiglu: g [M,N], w [N,I], gb [M,K2], a [R<=K2,I], gu [M,2I]");
+  auto dgu = torch::empty({M, 2 * I}, g_.options());
+  bcfl::G8Params g{g_.data_ptr(), w.data_ptr(), dgu.data_ptr(), g_.stride(0), w.stride(0), 2 * I, M, I, N};
+  g.b_col = 1;
+  g.epi = bcfl::EPI_SWIGLU_BWD;
+  g.aux = gu.data_ptr();
+  g.ldaux = gu.stride(0);
+  g.pair = I;
+  g.kc = N;
+  g.bm = bcfl::g8_auto_bm(M, I, 1);
+  g.A2 = gb.data_ptr();
+  g.B2 = a.data_ptr();
+  g.lda2 = gb.stride(0);
+  g.ldb2 = a.stride(0);
+  g.K2 = K2;
+  g.K2rows = R;
+  check_rc(bcfl::launch_g8(g, stream()), "lora_dgrad_swiglu");
+  return dgu;
+}
+
 // Tall-skinny LoRA products (skinny.hip): out[M, Cz] = scale * X[M, K] W[R, K]^T (columns
 // R..Cz-1 zero: the padded tail operand of lora_fwd / lora_dgrad) and out[R, N] = scale *
 // P[M, R]^T X[M, N]; both HBM-bound single passes over X with split fp32 partials
@@ -982,6 +1035,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_fwd", &rope_fwd);
+  m.def("lora_fwd_swiglu", &lora_fwd_swiglu);
+  m.def("lora_dgrad_swiglu", &lora_dgrad_swiglu);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("adamw", &adamw);

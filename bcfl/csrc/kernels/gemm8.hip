@@ -102,13 +102,15 @@ struct G8Op {
   // A_lo(t + 2), A_hi(t + 2), ...), so it costs no extra VGPRs in the pipelined loop
   const bf16_t* base2;
   int64_t ld2;
-  int i02, nv2, ke2, kt0, ktb;
+  int i02, nv2, ke2, kt0, ktb, hoff2;
   int tid_;
 
-  // ROW: base = rows [i0, i0 + n_rows) of a [*, ld] matrix, K range starts at k0 (elements)
+  // ROW: base = rows [i0, i0 + n_rows) of a [*, ld] matrix, K range starts at k0 (elements);
+  //      half-tile 1 starts `hoff` rows below half-tile 0 (H; the paired block's offset for the
+  //      SwiGLU gate|up tiles)
   // COL: base = k-rows [k0, k_end) of a [*, ld] matrix, columns from i0
   __device__ __forceinline__ void init(const bf16_t* base, int64_t ld, int i0, int n_valid, int k0,
-                                       int k_end, int tid) {
+                                       int k_end, int tid, int hoff = H) {
     if constexpr (!COL) {
       rs = buf_rsrc(base, ((int64_t)i0 * ld + k0) * 2, (int64_t)n_valid * ld * 2 - (int64_t)k0 * 2);
       kbytes = 64 * 2;
@@ -119,7 +121,7 @@ struct G8Op {
           const int idx = j * T8 + tid;
           const int r = (idx >> 3);
           const int c = (idx & 7) ^ ((r >> 1) & 7);
-          voff[h][j] = (int)((int64_t)(h * H + r) * ld * 2) + c * 16;
+          voff[h][j] = (int)((int64_t)(h * hoff + r) * ld * 2) + c * 16;
         }
     } else {
       rs = buf_rsrc(base, (int64_t)k0 * ld * 2, (int64_t)(k_end - k0) * ld * 2);
@@ -139,7 +141,7 @@ struct G8Op {
   // the tail segment: K-tiles [ktiles0, ...) read `base` from its k 0 (COL: k-rows [0, k_end),
   // rows past k_end zero-filled by the range check; ROW: zero-padded columns)
   __device__ __forceinline__ void init2(const bf16_t* base, int64_t ld, int i0, int n_valid,
-                                        int k_end, int tid, int ktiles0) {
+                                        int k_end, int tid, int ktiles0, int hoff = H) {
     if constexpr (TAIL) {
       base2 = base;
       ld2 = ld;
@@ -148,13 +150,14 @@ struct G8Op {
       ke2 = k_end;
       kt0 = ktiles0;
       tid_ = tid;
+      hoff2 = hoff;
     }
   }
   // issue the DMA of half-tile h of K-tile kt into LDS byte offset dst (wave w's 1-KiB pieces)
   __device__ __forceinline__ void dma(char* smem, int dst, int h, int kt, int w) {
     if constexpr (TAIL) {
       if (kt >= kt0 && ktb == 0) {  // workgroup-uniform, once per tile
-        init(base2, ld2, i02, nv2, 0, ke2, tid_);
+        init(base2, ld2, i02, nv2, 0, ke2, tid_, hoff2);
         ktb = kt0;
       }
       kt -= ktb;
@@ -224,6 +227,8 @@ template <int BM, bool ACOL, bool BCOL, int EPI, int ACT, bool PERSIST, bool TAI
 __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   using C = G8<BM, ACOL, BCOL, EPI, ACT>;
   constexpr int TI = C::TI, TJ = C::TJ, QM = C::QM, QN = C::QN, HA = C::HA, HB = C::HB;
+  constexpr bool PAIR = EPI == EPI_SWIGLU;
+  static_assert(!PAIR || !BCOL, "SwiGLU pairing: ROW B (forward) only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- tile / split assignment (XCD-aware: each XCD walks a contiguous range of tiles) -------
@@ -253,7 +258,9 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
     TileC c;
     c.split = L - tile * p.splits;
     c.m0 = (tile / tilesN) * BM;
-    c.n0 = (tile % tilesN) * BN8;
+    // SwiGLU forward: output tile t covers gate columns [128 t, 128 t + 128) (B half 0) and the
+    // same up columns (B half 1, `pair` rows further): each wave holds gate and up of its columns
+    c.n0 = (tile % tilesN) * (PAIR ? HB : BN8);
     c.kbeg = c.split * p.kc;
     c.kend = min(p.K, c.kbeg + p.kc);
     c.nt = ((c.kend - c.kbeg + 127) / 128) * 2;  // K-tiles, even
@@ -275,13 +282,16 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
   auto init_ops = [&](const TileC& c) {
     if constexpr (!ACOL) opA.init(A, p.lda, c.m0, min(BM, p.M - c.m0), c.kbeg, c.kend, tid);
     else opA.init(A, p.lda, c.m0, 0, c.kbeg, c.kend, tid);
-    if constexpr (!BCOL) opB.init(B, p.ldb, c.n0, min(BN8, p.N - c.n0), c.kbeg, c.kend, tid);
+    if constexpr (PAIR) opB.init(B, p.ldb, c.n0, p.pair + HB, c.kbeg, c.kend, tid, p.pair);
+    else if constexpr (!BCOL) opB.init(B, p.ldb, c.n0, min(BN8, p.N - c.n0), c.kbeg, c.kend, tid);
     else opB.init(B, p.ldb, c.n0, 0, c.kbeg, c.kend, tid);
     if constexpr (TAIL) {  // splits == 1: the base segment is K-tiles [0, K / 64)
       static_assert(!ACOL, "tail segment: ROW A operand only");
       const int kt0 = p.K / 64;
       opA.init2(reinterpret_cast<const bf16_t*>(p.A2), p.lda2, c.m0, min(BM, p.M - c.m0), p.K2, tid, kt0);
-      if constexpr (!BCOL)
+      if constexpr (PAIR)
+        opB.init2(reinterpret_cast<const bf16_t*>(p.B2), p.ldb2, c.n0, p.pair + HB, p.K2, tid, kt0, p.pair);
+      else if constexpr (!BCOL)
         opB.init2(reinterpret_cast<const bf16_t*>(p.B2), p.ldb2, c.n0, min(BN8, p.N - c.n0), p.K2, tid, kt0);
       else
         opB.init2(reinterpret_cast<const bf16_t*>(p.B2), p.ldb2, c.n0, 0, p.K2rows, tid, kt0);
@@ -484,17 +494,75 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
           }
       }
     }
+    // accumulator quadrant (a, bh) -> the wave's slab; 8 consecutive columns of slab row rr back
+    auto put = [&](int a, int bh) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            slab[(16 * i + (lane >> 4) * 4 + r) * LDF + 16 * j + (lane & 15)] = acc[a][bh][i][j][r];
+    };
+    auto get = [&](int rr, float (&v)[8]) {
+      if constexpr (PERSIST) {
+        // asm reads: the compiler would drain the next tile's DMA (vmcnt(0)) in front of a
+        // C++ LDS read while it is in flight
+        const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(slab + rr * LDF + cc);
+        f32x4_t lo, hi;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(ad) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(hi) : "v"(ad) : "memory");
+        lgk_wait<0>();
+        reg_fence(lo);
+        reg_fence(hi);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lo[e];
+          v[4 + e] = hi[e];
+        }
+      } else {
+        Vec8<float>::load(slab + rr * LDF + cc, v);
+      }
+    };
+    if constexpr (PAIR) {
+      // SwiGLU forward: the wave's gate (bh 0) and up (bh 1) quadrants cover the same columns
+      constexpr int NP = QM / RPP;
+      const int n = c.n0 + wc * QN + cc;  // gate column; the up column is pair + n
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        float gv[NP][8];
+        put(a, 0);
+#pragma unroll
+        for (int ps = 0; ps < NP; ++ps) get(rr0 + ps * RPP, gv[ps]);
+        put(a, 1);
+#pragma unroll
+        for (int ps = 0; ps < NP; ++ps) {
+          const int rr = rr0 + ps * RPP;
+          const int m = c.m0 + a * HA + wr * QM + rr;
+          float u[8];
+          get(rr, u);
+          if (m < p.M) {
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {  // the projection as stored (bf16), then silu(g) u
+              const float g = bf2f(f2bf(gv[ps][e]));
+              u[e] = bf2f(f2bf(u[e]));
+              gv[ps][e] = g;
+              o[e] = g / (1.f + __expf(-g)) * u[e];
+            }
+            Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + n, gv[ps]);
+            Vec8<bf16_t>::store(aux + (int64_t)m * p.ldaux + p.pair + n, u);
+            Vec8<bf16_t>::store(Cp + (int64_t)m * p.ldc + n, o);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int bh = 0; bh < 2; ++bh) {
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              slab[(16 * i + (lane >> 4) * 4 + r) * LDF + 16 * j + (lane & 15)] = acc[a][bh][i][j][r];
+        put(a, bh);
         const int n = c.n0 + bh * HB + wc * QN + cc;
         const float* bv = bvs[bh];
 #pragma unroll
@@ -502,24 +570,7 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
           const int rr = rr0 + ps * RPP;
           const int m = c.m0 + a * HA + wr * QM + rr;
           float v[8];
-          if constexpr (PERSIST) {
-            // asm reads: the compiler would drain the next tile's DMA (vmcnt(0)) in front of a
-            // C++ LDS read while it is in flight
-            const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(slab + rr * LDF + cc);
-            f32x4_t lo, hi;
-            asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(ad) : "memory");
-            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(hi) : "v"(ad) : "memory");
-            lgk_wait<0>();
-            reg_fence(lo);
-            reg_fence(hi);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[e] = lo[e];
-              v[4 + e] = hi[e];
-            }
-          } else {
-            Vec8<float>::load(slab + rr * LDF + cc, v);
-          }
+          get(rr, v);
           if (m < p.M) {
             if constexpr (EPI == EPI_PARTIAL) {
               float* dst = p.part + ((int64_t)c.split * p.M + m) * p.ldc + n;
@@ -544,6 +595,18 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
                 Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, rv);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] += rv[e];
+              } else if constexpr (EPI == EPI_SWIGLU_BWD) {  // dA -> (d gate, d up)
+                float gg[8], uu[8], du[8];
+                Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + n, gg);
+                Vec8<bf16_t>::load(aux + (int64_t)m * p.ldaux + p.pair + n, uu);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  const float d = bf2f(f2bf(v[e]));  // dA as the unfused path stores it
+                  const float sg = 1.f / (1.f + __expf(-gg[e]));
+                  du[e] = d * (gg[e] * sg);
+                  v[e] = d * uu[e] * sg * (1.f + gg[e] * (1.f - sg));
+                }
+                Vec8<bf16_t>::store(Cp + (int64_t)m * p.ldc + p.pair + n, du);
               } else if constexpr (EPI == EPI_ACCUM) {
                 float ov[8];
                 Vec8<bf16_t>::load(Cp + (int64_t)m * p.ldc + n, ov);
@@ -657,6 +720,10 @@ int g8_dispatch_tail(const G8Params& p, hipStream_t s, int nwg) {
     hipLaunchKernelGGL((g8_kernel<BM, false, BCOL, EPI_STORE, 0, PERSIST, true>), grid, block, lds, s, p);
   else if (p.epi == EPI_RESID && !BCOL)
     hipLaunchKernelGGL((g8_kernel<BM, false, false, EPI_RESID, 0, PERSIST, true>), grid, block, lds, s, p);
+  else if (p.epi == EPI_SWIGLU && !BCOL)
+    hipLaunchKernelGGL((g8_kernel<BM, false, false, EPI_SWIGLU, 0, PERSIST, true>), grid, block, lds, s, p);
+  else if (p.epi == EPI_SWIGLU_BWD && BCOL)
+    hipLaunchKernelGGL((g8_kernel<BM, false, true, EPI_SWIGLU_BWD, 0, PERSIST, true>), grid, block, lds, s, p);
   else
     return -4;
   return 0;
@@ -761,9 +828,14 @@ int g8_supported(const G8Params& p) {
   if (p.lda % 8 || p.ldb % 8 || p.ldc % 8) return -2;
   if ((p.epi == EPI_BIAS_ACT || p.epi == EPI_DACT) && (!p.aux || p.ldaux % 8)) return -3;
   if (p.epi == EPI_PARTIAL && !p.part) return -3;
+  if ((p.epi == EPI_SWIGLU || p.epi == EPI_SWIGLU_BWD) && p.K2 <= 0) return -4;  // LoRA path only
   if (p.K2 > 0) {  // tail segment: one split, ROW A2, K2 a whole number of K-tile pairs
     if (p.a_col || p.splits != 1 || p.K2 % 128 || !p.A2 || !p.B2 || p.lda2 % 8 || p.ldb2 % 8) return -3;
-    if (p.epi != EPI_STORE && !(p.epi == EPI_RESID && !p.b_col && p.aux && p.ldaux % 8 == 0))
+    const bool aux_ok = p.aux && p.ldaux % 8 == 0;
+    const bool pair_ok = p.pair > 0 && p.pair % 128 == 0 && aux_ok;
+    if (!(p.epi == EPI_STORE || (p.epi == EPI_RESID && !p.b_col && aux_ok) ||
+          (p.epi == EPI_SWIGLU && !p.b_col && pair_ok && p.N == 2 * p.pair) ||
+          (p.epi == EPI_SWIGLU_BWD && p.b_col && pair_ok && p.N == p.pair)))
       return -4;
     if (p.b_col && (p.K2rows <= 0 || p.K2rows > p.K2)) return -3;
   }

@@ -132,8 +132,12 @@ int skinny_ptx_splits(int M, int N, int* mc);
 int launch_skinny_ptx(const SkinnyParams& p, hipStream_t s);   // out = scale W^T X
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
+// RESID: C = A B (+ tail) + aux (residual). SWIGLU (gate|up forward, ROW B = [gate; up] with the
+// up block `pair` rows below the gate block): aux[M, 2 pair] = the bf16 projection [gate | up],
+// C[M, pair] = silu(gate) * up. SWIGLU_BWD (down-projection dgrad, C = dgu [M, 2 pair]): with
+// dA = A B (+ tail) and aux = [gate | up], C[:, n] = dA up silu'(gate), C[:, pair + n] = dA silu(gate).
 enum LinearEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_ACT = 2, EPI_DACT = 3, EPI_ACCUM = 4,
-                 EPI_PARTIAL = 5, EPI_RESID = 6 };  // RESID: C = A B (+ tail) + aux (residual)
+                 EPI_PARTIAL = 5, EPI_RESID = 6, EPI_SWIGLU = 7, EPI_SWIGLU_BWD = 8 };
 struct LinearParams {
   const void* A;       // [M, K] bf16, row stride lda
   const void* B;       // NT: [N, K] (ldb);  NN: [K, N] (ldb)
@@ -181,6 +185,7 @@ struct G8Params {
   const void* B2 = nullptr;
   int64_t lda2 = 0, ldb2 = 0;
   int K2 = 0, K2rows = 0;
+  int pair = 0;                  // EPI_SWIGLU / EPI_SWIGLU_BWD: the intermediate size I
 };
 int g8_supported(const G8Params& p);  // 0 = launchable
 int g8_auto_bm(int M, int N, int splits);

@@ -83,6 +83,11 @@ class DriftCorrection:
         self.stale_compensation = "none"
         self._pending: Dict[int, Optional[tuple]] = {}
         self.cv: Dict[int, torch.Tensor] = {}   # exchange mode: own control variate c_i
+        # exchange mode: per-client buffers that already hold the round-start model (+ the
+        # neighbours' updates applied on arrival) — the delta-exchange gossip's start records;
+        # when set, cv does not keep its own copy (one model-sized copy per round and one
+        # apply pass per arrival less)
+        self.start_of: Optional[Dict[int, torch.Tensor]] = None
         if self.enabled:
             for c in self.clients:
                 self.buf[c] = torch.zeros(numel, dtype=torch.float32, device=device)
@@ -110,7 +115,7 @@ class DriftCorrection:
             return
         opt.corr = self.buf[c] if self.ready[c] else None
         opt.corr_scale = self.scale
-        if self.exchange:
+        if self.exchange and self.start_of is None:
             if start is None:
                 raise ValueError("exchanged control variates need the round-start model")
             self.cv[c].copy_(start)
@@ -127,7 +132,11 @@ class DriftCorrection:
             return
         self.lr_sum[c] = float(lr_sum)
         if self.exchange:
-            ops.axpby_(self.cv[c], trained, -1.0 / lr_sum, 1.0 / lr_sum)
+            if self.start_of is not None:   # cv = (x_c - y_c) / L in one pass
+                ops.gossip_mix_(self.cv[c], [self.start_of[c], trained], 0.0,
+                                [1.0 / lr_sum, -1.0 / lr_sum])
+            else:
+                ops.axpby_(self.cv[c], trained, -1.0 / lr_sum, 1.0 / lr_sum)
             if self.ready[c]:
                 ops.axpby_(self.cv[c], self.buf[c], -self.scale, 1.0)
             return

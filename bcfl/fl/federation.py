@@ -215,6 +215,7 @@ class Federation:
                 self.server_mbox = MailboxFedAvg(self.flat.numel, self.device,
                                                  cfg.server_timeout_s, cfg.verify_updates)
         self.excluded: List[int] = []
+        self._lead_gone: Dict[int, int] = {}   # bounded staleness: neighbours given up on
         self.gossip: Optional[GossipEngine] = None
         if cfg.mode == "serverless" and not cfg.compat_chain:
             if cfg.topology_probe and self.rt.distributed:
@@ -269,6 +270,9 @@ class Federation:
                                            liveness_timeout=cfg.liveness_timeout,
                                            verify=cfg.verify_updates)
             if isinstance(self.gossip, MailboxGossip):
+                if self.gossip.exchange == "delta" and self.drift.exchange:
+                    # the gossip's round-start records double as the drift correction's x_c
+                    self.drift.start_of = self.gossip.start
                 # apply on arrival: neighbours' updates enter between local steps (delta exchange)
                 self.gossip.W_mid = mixing_matrix(self.nbrs, cfg.mixing)
                 self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival)
@@ -399,7 +403,7 @@ class Federation:
         enters at once (the AdamW steps that follow already use it)."""
         out = []
         if self.drift.exchange:
-            if self._phase.get(c) == "training":
+            if self._phase.get(c) == "training" and self.drift.start_of is None:
                 out.append((self.drift.cv[c], "model"))
             if self.drift.ready.get(c):
                 out.append((self.drift.buf[c], "aux"))
@@ -415,6 +419,50 @@ class Federation:
             g.poll(streams, self.client_param, self._mid_round_targets)
         else:
             g.poll(None, {self.local_clients[0]: self.flat.param}, self._mid_round_targets)
+
+    def _bound_lead(self, r: int) -> float:
+        """Bounded staleness (SSP) for the asynchronous mailbox gossip, ``gossip_max_lead`` = s > 0:
+        round r does not start while a live neighbour's newest applied update is more than s
+        rounds behind this rank's own last one (round r - 1); arriving updates are applied while
+        waiting. Ranks of equal speed never wait (a neighbour is at most ~1 round behind); ranks
+        that share a GPU, or a persistently slower one, are held within s rounds of each other —
+        without it 8 ranks time-sliced on one GPU drift 4-6 rounds apart and the fast ones train
+        mostly on their own label shard. The bound has its own liveness (the round-based
+        ``liveness_timeout`` would already have retired exactly the neighbours it must wait for):
+        a neighbour still behind after ``gossip_lead_timeout_s`` is skipped until it posts again.
+        Returns the seconds waited."""
+        s, g = int(self.cfg.gossip_max_lead), self.gossip
+        if s <= 0 or r == 0 or not isinstance(g, MailboxGossip) or not g.async_gossip:
+            return 0.0
+        posted = {}   # without apply-on-arrival: the newest round a neighbour has POSTED
+        gone = self._lead_gone
+
+        def seen(j):
+            return max(g.replica_round[j], posted.get(j, -1))
+
+        def lag():
+            for j in [j for j in gone if seen(j) > gone[j]]:
+                del gone[j]   # posted again: bounded again
+            return [j for j in g.remote_needed if j not in gone and seen(j) < r - 1 - s]
+        if not lag():
+            return 0.0
+        t0 = time.perf_counter()
+        while True:
+            late = lag()
+            if not late:
+                break
+            if time.perf_counter() - t0 > float(self.cfg.gossip_lead_timeout_s):
+                gone.update({j: seen(j) for j in late})
+                break
+            if g.apply_on_arrival:
+                self._gossip_poll()
+            else:
+                for j, h in g.transport.headers(late).items():
+                    nw = g.transport.newest(h)
+                    if nw is not None:
+                        posted[j] = nw[1].round
+            time.sleep(0.0005)
+        return time.perf_counter() - t0
 
     @contextlib.contextmanager
     def _client_rng(self, c: int):
@@ -1201,6 +1249,7 @@ class Federation:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
         need_prev = self.filter is not None or bool(cfg.inject_byzantine)
+        lead_wait = self._bound_lead(r)
         if self.outer.enabled:
             for c in self.local_clients:
                 self.outer.begin(c, self.client_master[c] if self.multi else self.flat.master)
@@ -1286,7 +1335,8 @@ class Federation:
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
                 "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
                 "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
-                "stale_max": info.get("stale_max", 0.0), "wait_s": info.get("wait_s", 0.0),
+                "stale_max": info.get("stale_max", 0.0),
+                "wait_s": info.get("wait_s", 0.0) + lead_wait, "lead_wait_s": lead_wait,
                 "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
                 "rejected_msgs": info.get("rejected_msgs", 0.0)}
 

@@ -115,11 +115,11 @@ class LlamaLayer(nn.Module):
         else:
             x = x + ops.linear(ctx, self.o_weight)
         h2 = ops.rmsnorm(x, self.post_ln, c.rms_norm_eps)
-        gu = (self.lora_gate_up.fused(h2, self.gate_up_weight) if self.lora
-              else ops.linear(h2, self.gate_up_weight))
-        a = ops.swiglu(gu)
-        if self.lora:
-            return self.lora_down.fused(a, self.down_weight, residual=x)
+        if self.lora:   # SwiGLU and the residual add in the projections' GEMM epilogues
+            gl, dl = self.lora_gate_up, self.lora_down
+            return ops.lora_swiglu_mlp(h2, self.gate_up_weight, gl.A, list(gl.B), gl.scale,
+                                       self.down_weight, dl.A, list(dl.B), dl.scale, x)
+        a = ops.swiglu(ops.linear(h2, self.gate_up_weight))
         return x + ops.linear(a, self.down_weight)
 
 

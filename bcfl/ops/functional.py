@@ -24,7 +24,7 @@ from ._native import available as native_available, native, use_native
 
 __all__ = ["bias_dropout_add_layernorm", "layernorm", "bias_act", "varlen_attention",
            "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "wgrad",
-           "linear_act", "linear_after_act", "gemm_supported", "lora_linear", "xent_stats_",
+           "linear_act", "linear_after_act", "gemm_supported", "lora_linear", "lora_swiglu_mlp", "xent_stats_",
            "query_subset_attention", "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad"]
 
 
@@ -492,6 +492,106 @@ def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, bs, s: float,
     d = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
     y = linear(x, w) + d * s
     return y if residual is None else residual + y
+
+
+def _lora_skinny_operands(x2, a, bs, s):
+    """xa = x A^T ([M, k2], zero past n r) and s Bbd zero-padded to k2 columns."""
+    nr = a.shape[0]
+    k2 = _lora_k2(nr)
+    xa = native().skinny_xwt(x2, a, k2, 1.0)
+    bb = a.new_zeros(sum(int(b.shape[0]) for b in bs), k2)
+    torch.mul(torch.block_diag(*bs), s, out=bb[:, :nr])
+    return xa, bb
+
+
+def _lora_db(full_t: torch.Tensor, sizes, nr: int):
+    """dB_i from the stacked s xa^T g [n r, N] (block i = rows i r.., columns of output block i)."""
+    r = nr // len(sizes)
+    out, o = [], 0
+    for i, n in enumerate(sizes):
+        out.append(full_t[i * r:(i + 1) * r, o:o + n].t().contiguous())
+        o += n
+    return out
+
+
+class _LoRASwiGLUMLP(torch.autograd.Function):
+    """Llama MLP with LoRA on both projections and SwiGLU inside the GEMM epilogues:
+
+        gu  = x Wgu^T + s xa_g Bbd_g^T           act = silu(gate) * up     (ONE GEMM: EPI_SWIGLU)
+        y   = res + act Wd^T + s xa_d Bbd_d^T                              (ONE GEMM: EPI_RESID)
+      backward:
+        dgu = SwiGLU'(gu) . (g Wd + gbs_d Ad)    (ONE GEMM: EPI_SWIGLU_BWD; dA never stored)
+        dx  = dgu Wgu + gbs_g Ag                 (tail-segment dgrad)
+
+    versus _LoRALinear + ops.swiglu it saves the SwiGLU forward pass (read gu, write act) and
+    backward pass (read dA and gu, write dgu) and the dA tensor (config 5: swiglu fwd + bwd were
+    2.8 % of kernel time, profiles/config5_kernel_stats_r3.md). The low-rank products run on
+    skinny.hip (see :class:`_LoRALinear`). Reference: the HF LlamaMLP
+    ``down_proj(act_fn(gate_proj(x)) * up_proj(x))`` the north star's config 5 trains with PEFT."""
+
+    @staticmethod
+    def forward(ctx, x, wgu, agu, sgu, ngu, wd, ad, sd, nd, res, *bs):
+        C = native()
+        bgu, bd = bs[:ngu], bs[ngu:]
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        res2 = res.reshape(-1, wd.shape[0]).contiguous()
+        xa_g, bb_g = _lora_skinny_operands(x2, agu, bgu, sgu)
+        act, gu = C.lora_fwd_swiglu(x2, wgu, xa_g, bb_g)
+        xa_d, bb_d = _lora_skinny_operands(act, ad, bd, sd)
+        y = C.lora_fwd(act, wd, xa_d, bb_d, res2)
+        ctx.save_for_backward(x2, wgu, agu, xa_g, bb_g, gu, act, wd, ad, xa_d, bb_d)
+        ctx.s = (sgu, sd)
+        ctx.sizes = (tuple(int(b.shape[0]) for b in bgu), tuple(int(b.shape[0]) for b in bd))
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], wd.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, wgu, agu, xa_g, bb_g, gu, act, wd, ad, xa_d, bb_d = ctx.saved_tensors
+        (sgu, sd), (zgu, zd) = ctx.s, ctx.sizes
+        C = native()
+        g2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        nrd, nrg = ad.shape[0], agu.shape[0]
+        gbs_d = C.skinny_xwt(g2, bb_d[:, :nrd].t().contiguous(), xa_d.shape[1], 1.0)
+        dgu = C.lora_dgrad_swiglu(g2, wd, gbs_d, ad, gu)
+        dad = C.skinny_ptx(gbs_d[:, :nrd], act, 1.0)
+        dbd = _lora_db(C.skinny_ptx(xa_d[:, :nrd], g2, sd), zd, nrd)
+        gbs_g = C.skinny_xwt(dgu, bb_g[:, :nrg].t().contiguous(), xa_g.shape[1], 1.0)
+        dx = C.lora_dgrad(dgu, wgu, gbs_g, agu).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dag = C.skinny_ptx(gbs_g[:, :nrg], x2, 1.0)
+        dbg = _lora_db(C.skinny_ptx(xa_g[:, :nrg], dgu, sgu), zgu, nrg)
+        return (dx, None, dag, None, None, None, dad, None, None, gy, *dbg, *dbd)
+
+
+# BCFL_LORA_MLP_FUSED=0: gate|up and down as two _LoRALinear + ops.swiglu (A/B)
+_LORA_MLP_FUSED = os.environ.get("BCFL_LORA_MLP_FUSED", "1") == "1"
+
+
+def _lora_mlp_fused_ok(x: torch.Tensor, wgu, agu, wd, ad) -> bool:
+    M, H = x.numel() // x.shape[-1], x.shape[-1]
+    I = wd.shape[1]
+    return (_LORA_MLP_FUSED and use_native(x, "lora") and x.dtype == torch.bfloat16
+            and not wgu.requires_grad and not wd.requires_grad and wgu.is_contiguous()
+            and wd.is_contiguous() and agu.is_contiguous() and ad.is_contiguous()
+            and wgu.shape == (2 * I, H) and wd.shape[0] == H and M >= WGRAD_MIN_ROWS
+            and I % 256 == 0 and H % 256 == 0
+            and _skinny_ok(agu.shape[0], M, 2 * I, H) and _skinny_ok(ad.shape[0], M, H, I)
+            and bool(native().lora_native_ok(M, 2 * I, H, False))
+            and bool(native().lora_native_ok(M, H, I, False))
+            and bool(native().lora_native_ok(M, I, H, True))
+            and bool(native().lora_native_ok(M, H, 2 * I, True)))
+
+
+def lora_swiglu_mlp(x: torch.Tensor, wgu: torch.Tensor, agu: torch.Tensor, bgu, sgu: float,
+                    wd: torch.Tensor, ad: torch.Tensor, bd, sd: float,
+                    residual: torch.Tensor) -> torch.Tensor:
+    """residual + down(swiglu(gate_up(x))) with LoRA adapters on both frozen projections
+    (:class:`_LoRASwiGLUMLP` on the GPU; elsewhere the two :func:`lora_linear` + :func:`swiglu`)."""
+    if _lora_mlp_fused_ok(x, wgu, agu, wd, ad):
+        return _LoRASwiGLUMLP.apply(x, wgu, agu, float(sgu), len(bgu), wd, ad, float(sd), len(bd),
+                                    residual, *bgu, *bd)
+    a = swiglu(lora_linear(x, wgu, agu, bgu, sgu))
+    return lora_linear(a, wd, ad, bd, sd, residual)
 
 
 def _use_linear_fn(x: torch.Tensor, w: torch.Tensor) -> bool:

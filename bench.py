@@ -110,6 +110,20 @@ def _launch_ranks(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _async_mix_desc(fed) -> str:
+    g = fed.gossip
+    delta = getattr(g, "exchange", "state") == "delta"
+    d = ("neighbours' cumulative updates applied once each" + (
+        ", on arrival between local steps" if getattr(g, "apply_on_arrival", False) else
+        ", at the round end") if delta else "newest complete snapshot of each neighbour")
+    lead = int(fed.cfg.gossip_max_lead)
+    d += (f"; bounded staleness: waits only while a neighbour is > {lead} rounds behind"
+          if lead > 0 and fed.rt.distributed else "; never waits")
+    if fed.drift.exchange:
+        d += " + exchanged SCAFFOLD control variates (stale-exact)"
+    return d
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -185,6 +199,7 @@ def main():
         ex = {"stale_rounds": [h.get("stale_rounds") for h in timed],
               "stale_max": max([float(h.get("stale_max") or 0.0) for h in timed] or [0.0]),
               "wait_s_total": sum(float(h.get("wait_s") or 0.0) for h in timed),
+              "lead_wait_s_total": sum(float(h.get("lead_wait_s") or 0.0) for h in timed),
               "torn": sum(float(h.get("torn") or 0.0) for h in timed),
               "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
               "mixed": sum(float(h.get("mixed") or 0.0) for h in timed)}
@@ -261,9 +276,7 @@ def main():
                        "gossip_mix": ("same-round snapshots (waits for every neighbour's "
                                       "round-r post)" if getattr(fed, "same_round_mix", False) else
                                       "same-round" if a.sync else
-                                      "newest complete snapshot, never waits" + (
-                                          " + exchanged SCAFFOLD control variates (stale-exact)"
-                                          if fed.drift.exchange else "")),
+                                      _async_mix_desc(fed)),
                        "train_samples_per_client": cfg.train_samples, "ledger": cfg.ledger,
                        "client_lanes_per_gpu": len(fed.lanes) or 1,
                        "micro_batches_per_step": fed.micro_split,

@@ -604,6 +604,76 @@ def test_lora_tail_gemms_match_fp32(M, N, K, nr):
     _close(dx, ref_dx, 5e-2, 2e-2)
 
 
+@pytest.mark.parametrize("M,H,I,nr", [(2048, 512, 768, 32), (8192, 1024, 1536, 32), (1500, 256, 512, 16)])
+def test_lora_swiglu_epilogues_match_fp32(M, H, I, nr):
+    """gemm8.hip EPI_SWIGLU: [gate|up] = x Wgu^T + xa bb^T with each output tile pairing gate
+    columns with the same up columns (B half-tile 1 read I rows further), act = silu(gate) up;
+    EPI_SWIGLU_BWD: dgu = SwiGLU'(gu) . (g Wd + gb Ad) with dA never stored. vs fp32 torch."""
+    torch.manual_seed(M + I)
+    C = ops.native()
+    k2 = -(-nr // 128) * 128
+    x = torch.randn(M, H, device=DEV).bfloat16()
+    wgu = (torch.randn(2 * I, H, device=DEV) * 0.05).bfloat16()
+    xa = torch.zeros(M, k2, device=DEV, dtype=torch.bfloat16)
+    xa[:, :nr] = torch.randn(M, nr, device=DEV).bfloat16()
+    bb = torch.zeros(2 * I, k2, device=DEV, dtype=torch.bfloat16)
+    bb[:, :nr] = (torch.randn(2 * I, nr, device=DEV) * 0.1).bfloat16()
+    act, gu = C.lora_fwd_swiglu(x, wgu, xa, bb)
+    ref_gu = x.float() @ wgu.float().t() + xa.float() @ bb.float().t()
+    _close(gu, ref_gu, 5e-2, 2e-2)
+    g_, u_ = gu.float()[:, :I], gu.float()[:, I:]      # the kernel's own bf16 projection
+    _close(act, torch.nn.functional.silu(g_) * u_, 2e-2, 2e-2)
+    wd = (torch.randn(H, I, device=DEV) * 0.05).bfloat16()
+    gy = torch.randn(M, H, device=DEV).bfloat16()
+    gb = torch.zeros(M, k2, device=DEV, dtype=torch.bfloat16)
+    gb[:, :nr] = torch.randn(M, nr, device=DEV).bfloat16()
+    ad = (torch.randn(nr, I, device=DEV) * 0.1).bfloat16()
+    dgu = C.lora_dgrad_swiglu(gy, wd, gb, ad, gu)
+    dA = (gy.float() @ wd.float() + gb[:, :nr].float() @ ad.float()).bfloat16().float()
+    sg = torch.sigmoid(g_)
+    ref_dg = dA * u_ * sg * (1 + g_ * (1 - sg))
+    ref_du = dA * g_ * sg
+    _close(dgu[:, :I], ref_dg, 5e-2, 2e-2)
+    _close(dgu[:, I:], ref_du, 5e-2, 2e-2)
+
+
+@pytest.mark.parametrize("T", [2048, 4096])
+def test_lora_swiglu_mlp_matches_unfused(T):
+    """ops.lora_swiglu_mlp (SwiGLU forward / backward in the GEMM epilogues, one autograd node for
+    the whole LoRA MLP) == two ops.lora_linear + ops.swiglu on the torch route: output and every
+    gradient (input, residual, both A's and all B's)."""
+    import os
+    from bcfl.ops import functional as F
+    torch.manual_seed(T)
+    H, I, r = 512, 768, 16
+    x0 = torch.randn(T, H, device=DEV).bfloat16()
+    r0 = torch.randn(T, H, device=DEV).bfloat16()
+    wgu = (torch.randn(2 * I, H, device=DEV) * 0.05).bfloat16()
+    wd = (torch.randn(H, I, device=DEV) * 0.05).bfloat16()
+    agu0 = (torch.randn(2 * r, H, device=DEV) * 0.05).bfloat16()
+    ad0 = (torch.randn(r, I, device=DEV) * 0.05).bfloat16()
+    bgu0 = [(torch.randn(I, r, device=DEV) * 0.05).bfloat16() for _ in range(2)]
+    bd0 = [(torch.randn(H, r, device=DEV) * 0.05).bfloat16()]
+    gy = torch.randn(T, H, device=DEV).bfloat16()
+    assert F._lora_mlp_fused_ok(x0, wgu, agu0, wd, ad0)
+    res = {}
+    for route in ("bcfl", "torch"):
+        os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "lora"
+        try:
+            x, rr = x0.clone().requires_grad_(True), r0.clone().requires_grad_(True)
+            agu, ad = agu0.clone().requires_grad_(True), ad0.clone().requires_grad_(True)
+            bgu = [b.clone().requires_grad_(True) for b in bgu0]
+            bd = [b.clone().requires_grad_(True) for b in bd0]
+            y = ops.lora_swiglu_mlp(x, wgu, agu, bgu, 2.0, wd, ad, bd, 2.0, rr)
+            y.backward(gy)
+            res[route] = [y, x.grad, rr.grad, agu.grad, ad.grad] + [b.grad for b in bgu + bd]
+        finally:
+            os.environ["BCFL_TORCH_OPS"] = ""
+    for i, (u, v) in enumerate(zip(res["bcfl"], res["torch"])):
+        err = ((u.float() - v.float()).norm() / v.float().norm()).item()
+        assert err < 2e-2, (i, err)
+
+
 @pytest.mark.parametrize("B,C", [(32, 2), (7, 41), (256, 40), (300, 3)])
 def test_xent_kernels_match_torch(B, C):
     torch.manual_seed(B + C)

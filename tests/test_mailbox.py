@@ -118,8 +118,10 @@ def test_mailbox_sync_equals_single_process(tmp_path):
 
 
 def test_mailbox_tamper_rejected_and_logged(tmp_path):
+    # test barrier: round r's posts land before round r + 1 fetches (on a loaded CPU rank 1 could
+    # otherwise finish all three rounds before rank 0's first post and accept nothing)
     res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"inject_tamper": [1], "num_rounds": 3})
+                    {"inject_tamper": [1], "num_rounds": 3}, None, True)
     # rank 0 rejects every (corrupted) update of client 1; rank 1 accepts client 0's
     assert int(res[0]["rejects"]) >= 1 and int(res[0]["accepts"]) == 0
     assert int(res[1]["rejects"]) == 0 and int(res[1]["accepts"]) >= 1
@@ -209,13 +211,31 @@ def test_mailbox_async_two_ranks_slow_peer_learn_label_shards(tmp_path):
     post (stale-exact c_hat). The round-3 alternative (state mixing of stale snapshots, mix-derived
     c') stayed near the majority rate (0.50 on MI355X, profiles/multirank_learning_r3.json)."""
     res = run_world(_learn_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"inject_slow": {1: 200.0}, "liveness_timeout": 6})
+                    {"inject_slow": {1: 200.0}, "liveness_timeout": 6, "gossip_max_lead": 0})
     _check_async_learning(res)
 
 
 @pytest.mark.slow
 def test_mailbox_async_four_ranks_learn_label_shards(tmp_path):
-    """Same with one client per rank (every neighbour remote: every mix is stale)."""
+    """Same with one client per rank (every neighbour remote: every mix is stale). Both tests run
+    UNBOUNDED (gossip_max_lead = 0: no rank ever waits); the default bound is pinned below."""
     res = run_world(_learn_worker, 4, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"num_rounds": 20, "liveness_timeout": 6})
+                    {"num_rounds": 20, "liveness_timeout": 6, "gossip_max_lead": 0})
     _check_async_learning(res)
+
+
+@pytest.mark.slow
+def test_mailbox_async_eight_ranks_bounded_lead_learn_label_shards(tmp_path):
+    """8 ranks on 8 CPU cores (time-sliced, so they drift apart the way 8 processes sharing one
+    GPU do): unbounded they end up 4-6 rounds apart and the fast ranks train mostly on their
+    own label shard (0.50-0.95 federation accuracy over repeated runs); the default bounded
+    staleness (FLConfig.gossip_max_lead = 2: no round starts while a live neighbour's newest
+    applied update is more than 2 rounds behind) keeps every rank learning."""
+    res = run_world(_learn_worker, 8, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"num_clients": 8, "num_rounds": 20})
+    for r in res:
+        assert not r["same_round"] and r["exchange"] and r["delta"]
+        assert float(r["acc"][-3:].max()) >= 0.9, r["acc"].tolist()
+        assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
+        assert float(r["wait"]) < 30.0   # the bound holds fast ranks back a little, never stalls
+
