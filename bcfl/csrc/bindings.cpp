@@ -863,6 +863,67 @@ Tensor skinny_ptx(Tensor pm, Tensor x, double scale) {
   return out;
 }
 
+// LoRA adapter B gradients straight from the stacked product: out[N, r] with out[o_b:o_b + n_b] =
+// scale * (P^T X)[b r:(b + 1) r, o_b:o_b + n_b]^T = adapter b's dB (contiguous row blocks; the
+// off-diagonal blocks are computed and dropped by the reduce, nothing else is materialised)
+Tensor skinny_ptx_bdiag(Tensor pm, Tensor x, std::vector<int64_t> sizes, double scale) {
+  check_gemm_operand(pm, "p");
+  check_gemm_operand(x, "x");
+  const int nb = (int)sizes.size();
+  TORCH_CHECK(nb >= 1 && nb <= 4 && pm.size(1) % nb == 0, "skinny_ptx_bdiag: 1..4 blocks of r columns");
+  const int M = x.size(0), N = x.size(1), R = pm.size(1), r = R / nb;
+  TORCH_CHECK(pm.size(0) == M && R <= 64 && R % 8 == 0 && N % 64 == 0,
+              "skinny_ptx_bdiag: p [M,R<=64, R%8==0], x [M,N%64==0]");
+  int mc = 0;
+  const int S = bcfl::skinny_ptx_splits(M, N, &mc);
+  const int RP = (R + 15) / 16 * 16;
+  auto part = torch::empty({S, RP, N}, x.options().dtype(torch::kFloat));
+  auto out = torch::empty({N, r}, x.options());
+  bcfl::SkinnyParams p{x.data_ptr(), x.stride(0), pm.data_ptr(), pm.stride(0), M, N, 0, R, S, mc,
+                       part.data_ptr<float>(), out.data_ptr(), r, 0, (float)scale};
+  p.bdr = r;
+  p.nblk = nb;
+  int o = 0;
+  for (int b = 0; b < nb; ++b) {
+    p.boff[b] = o;
+    o += (int)sizes[b];
+  }
+  p.boff[nb] = o;
+  for (int b = nb + 1; b < 5; ++b) p.boff[b] = o;
+  TORCH_CHECK(o == N, "skinny_ptx_bdiag: block sizes must sum to N");
+  check_rc(bcfl::launch_skinny_ptx(p, stream()), "skinny_ptx_bdiag");
+  return out;
+}
+
+// {bb [N, k2] = s Bbd zero-padded, bbt [n r, N] = bb[:, :n r]^T} from the adapters' B_b [o_b, r]
+std::vector<Tensor> lora_pack_b(std::vector<Tensor> bs, double s, int64_t k2) {
+  const int nb = (int)bs.size();
+  TORCH_CHECK(nb >= 1 && nb <= 4, "lora_pack_b: 1..4 adapters");
+  const int r = bs[0].size(1);
+  bcfl::LoraPackParams p{};
+  int o = 0;
+  for (int b = 0; b < nb; ++b) {
+    TORCH_CHECK(bs[b].is_cuda() && bs[b].is_contiguous() && bs[b].dim() == 2 && bs[b].size(1) == r &&
+                bs[b].scalar_type() == at::kBFloat16, "lora_pack_b: contiguous bf16 [o_b, r]");
+    p.B[b] = bs[b].data_ptr();
+    p.boff[b] = o;
+    o += bs[b].size(0);
+  }
+  p.boff[nb] = o;
+  TORCH_CHECK(nb * r <= k2, "lora_pack_b: n r > k2");
+  p.nblk = nb;
+  p.r = r;
+  p.N = o;
+  p.k2 = (int)k2;
+  p.s = (float)s;
+  auto bb = torch::empty({o, k2}, bs[0].options());
+  auto bbt = torch::empty({nb * r, o}, bs[0].options());
+  p.bb = bb.data_ptr();
+  p.bbt = bbt.data_ptr();
+  check_rc(bcfl::launch_lora_pack_b(p, stream()), "lora_pack_b");
+  return {bb, bbt};
+}
+
 // whether lora_fwd (nn = false: M, N outputs, K) / lora_dgrad (nn = true) take a shape
 bool lora_native_ok(int64_t M, int64_t N, int64_t K, bool nn) {
   bcfl::G8Params g{nullptr, nullptr, nullptr, 8, 8, 8, (int)M, (int)N, (int)K};
@@ -1036,6 +1097,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_fwd", &rope_fwd);
   m.def("lora_fwd_swiglu", &lora_fwd_swiglu);
+  m.def("skinny_ptx_bdiag", &skinny_ptx_bdiag);
+  m.def("lora_pack_b", &lora_pack_b);
   m.def("lora_dgrad_swiglu", &lora_dgrad_swiglu);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

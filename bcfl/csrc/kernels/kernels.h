@@ -125,11 +125,27 @@ struct SkinnyParams {
   int64_t ldo;
   int Cz;
   float scale;
+  // ptx only, LoRA dB mode (bdr > 0): out is [N, bdr] with out[n, j] = scale * (W^T X)[blk(n) bdr
+  // + j, n], blk(n) the block with boff[b] <= n < boff[b + 1] — the diagonal blocks of the stacked
+  // product, transposed: out[boff[b]:boff[b + 1]] IS adapter b's B gradient (contiguous rows)
+  int bdr = 0, nblk = 0;
+  int boff[5] = {0, 0, 0, 0, 0};
 };
 int skinny_xwt_splits(int M, int K, int* kc);
 int launch_skinny_xwt(const SkinnyParams& p, hipStream_t s);   // out = scale X W^T (+ zero cols)
 int skinny_ptx_splits(int M, int N, int* mc);
 int launch_skinny_ptx(const SkinnyParams& p, hipStream_t s);   // out = scale W^T X
+// LoRA adapter packing: bb[N, k2] = s Bbd zero-padded (block b of r columns holds B_b [o_b, r] at
+// rows boff[b]..), bbt[nr, N] = bb[:, :nr]^T (the operand of the backward's g (s Bbd) product)
+struct LoraPackParams {
+  const void* B[4];
+  int boff[5];
+  int nblk, r, N, k2;
+  float s;
+  void* bb;
+  void* bbt;
+};
+int launch_lora_pack_b(const LoraPackParams& p, hipStream_t s);
 
 // ---- linear.hip: dense-layer GEMMs with fused epilogues ------------------------------------------
 // RESID: C = A B (+ tail) + aux (residual). SWIGLU (gate|up forward, ROW B = [gate; up] with the

@@ -21,6 +21,8 @@
 //               (64 columns, M slice), double-buffered tiles; split-M fp32 partials.
 //   reduce:     the slices summed in a fixed order (deterministic), bf16 out, optional zero
 //               columns (the tail-segment padding the fused LoRA GEMMs of gemm8.hip read).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "lds_dma.h"
@@ -234,7 +236,60 @@ __global__ __launch_bounds__(256) void skinny_reduce_cols_kernel(const float* __
   out[(int64_t)c * ldo + n] = f2bf(v * scale);
 }
 
+// LoRA dB: out[n, j] = bf16(scale * sum_s part[s, blk(n) r + j, n]), n fastest across threads
+// (coalesced partial reads)
+__global__ __launch_bounds__(256) void skinny_reduce_bdiag_kernel(const float* __restrict__ part,
+                                                                  int S, int RP, int N, int r,
+                                                                  int nblk, int4 lo, int hi4,
+                                                                  float scale, bf16_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)r * N) return;
+  const int j = (int)(i / N), n = (int)(i % N);
+  const int bo[5] = {lo.x, lo.y, lo.z, lo.w, hi4};
+  int b = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q) b += (q < nblk && n >= bo[q]) ? 1 : 0;
+  const int c = b * r + j;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[((int64_t)s * RP + c) * N + n];
+  out[(int64_t)n * r + j] = f2bf(v * scale);
+}
+
+__global__ __launch_bounds__(256) void lora_pack_b_kernel(LoraPackParams p) {
+  const int nr = p.nblk * p.r;
+  const int64_t tot1 = (int64_t)p.N * p.k2, tot2 = (int64_t)nr * p.N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < tot1 + tot2;
+       i += (int64_t)gridDim.x * 256) {
+    int n, c;
+    if (i < tot1) {
+      n = (int)(i / p.k2);
+      c = (int)(i % p.k2);
+    } else {
+      c = (int)((i - tot1) / p.N);
+      n = (int)((i - tot1) % p.N);
+    }
+    float v = 0.f;
+    if (c < nr) {
+      const int b = c / p.r;
+      if (n >= p.boff[b] && n < p.boff[b + 1])
+        v = p.s * bf2f(reinterpret_cast<const bf16_t*>(p.B[b])[(int64_t)(n - p.boff[b]) * p.r + (c - b * p.r)]);
+    }
+    if (i < tot1) reinterpret_cast<bf16_t*>(p.bb)[i] = f2bf(v);
+    else reinterpret_cast<bf16_t*>(p.bbt)[(int64_t)c * p.N + n] = f2bf(v);
+  }
+}
+
 }  // namespace
+
+int launch_lora_pack_b(const LoraPackParams& p, hipStream_t s) {
+  if (p.nblk < 1 || p.nblk > 4 || p.r < 1 || p.nblk * p.r > p.k2 || p.boff[0] != 0 ||
+      p.boff[p.nblk] != p.N)
+    return -1;
+  const int64_t tot = (int64_t)p.N * p.k2 + (int64_t)p.nblk * p.r * p.N;
+  const int grid = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(lora_pack_b_kernel, dim3(grid), dim3(256), 0, s, p);
+  return 0;
+}
 
 int skinny_xwt_splits(int M, int K, int* kc) {
   // ~2 slices per CU's worth of 32-row waves: at M = 8k, 256 row waves x S slices
@@ -288,6 +343,15 @@ int launch_skinny_ptx(const SkinnyParams& p, hipStream_t s) {
     case 2: hipLaunchKernelGGL(skinny_ptx_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)p.W, p.ldw, (const bf16_t*)p.X, p.ldx, p.M, p.N, p.R, p.kc, p.part); break;
     case 3: hipLaunchKernelGGL(skinny_ptx_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)p.W, p.ldw, (const bf16_t*)p.X, p.ldx, p.M, p.N, p.R, p.kc, p.part); break;
     default: hipLaunchKernelGGL(skinny_ptx_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)p.W, p.ldw, (const bf16_t*)p.X, p.ldx, p.M, p.N, p.R, p.kc, p.part); break;
+  }
+  if (p.bdr > 0) {  // LoRA dB: the diagonal blocks, transposed into [N, r]
+    if (p.nblk < 1 || p.nblk > 4 || p.nblk * p.bdr != p.R || p.boff[p.nblk] != p.N) return -2;
+    const int64_t tot = (int64_t)p.bdr * p.N;
+    hipLaunchKernelGGL(skinny_reduce_bdiag_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                       p.part, p.S, 16 * RB, p.N, p.bdr, p.nblk,
+                       make_int4(p.boff[0], p.boff[1], p.boff[2], p.boff[3]), p.boff[4], p.scale,
+                       (bf16_t*)p.out);
+    return 0;
   }
   const int64_t tot = (int64_t)p.R * p.N;
   hipLaunchKernelGGL(skinny_reduce_cols_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,

@@ -367,7 +367,6 @@ class _LoRALinear(torch.autograd.Function):
             x2 = x2.contiguous()
         M, N, K = x2.shape[0], w.shape[0], w.shape[1]
         nr = a.shape[0]
-        bbd = torch.block_diag(*bs)                       # [N, n r]
         fused = (w.is_contiguous() and a.is_contiguous() and nr <= _LORA_PAD and M >= WGRAD_MIN_ROWS
                  and N % 256 == 0 and K % 256 == 0
                  and _lora_tail_ok(M, N, K, False, x2, w) and _lora_tail_ok(M, K, N, True, x2, w))
@@ -380,15 +379,14 @@ class _LoRALinear(torch.autograd.Function):
             if res2.stride(-1) != 1 or res2.stride(0) % 8:
                 res2 = res2.contiguous()
         if ctx.skinny:
-            k2 = _lora_k2(nr)
-            xa_f = native().skinny_xwt(x2, a, k2, 1.0)      # [M, k2], columns >= n r zero
-            bb_p = w.new_zeros(N, k2)
-            torch.mul(bbd, s, out=bb_p[:, :nr])
+            # xa [M, k2] (columns >= n r zero), s Bbd padded + its transpose (one packing kernel)
+            xa_f, bb_p, bbt = _lora_skinny_operands(x2, a, bs, s)
             # the residual stream add rides on the GEMM epilogue (EPI_RESID)
             y = native().lora_fwd(x2, w, xa_f, bb_p, res2)
             res2 = None
-            ctx.save_for_backward(x2, w, a, xa_f, bb_p)
+            ctx.save_for_backward(x2, w, a, xa_f, bbt)
         elif fused:
+            bbd = torch.block_diag(*bs)                   # [N, n r]
             k2 = _lora_k2(nr)
             if _LORA_G8_SKINNY:
                 a_p = a.new_zeros(_LORA_PAD, K)
@@ -402,6 +400,7 @@ class _LoRALinear(torch.autograd.Function):
             y = native().lora_fwd(x2, w, xa_f[:, :k2], bb_p[:, :k2])
             ctx.save_for_backward(x2, w, a, xa_f, bb_p)
         else:
+            bbd = torch.block_diag(*bs)                   # [N, n r]
             xa = x2 @ a.t()                               # [M, n r]
             y = torch.mm(xa * s, bbd.t())                 # scale on the [M, n r] side
             if w.is_contiguous() and _native_accum_ok(M, N, K, False, x2, w, y):
@@ -423,22 +422,17 @@ class _LoRALinear(torch.autograd.Function):
         dx = da = None
         dbs = [None] * len(sizes)
         if ctx.skinny:
-            x2, w, a, xa_f, bb_p = ctx.saved_tensors
+            x2, w, a, xa_f, bbt = ctx.saved_tensors
             nr, k2 = a.shape[0], xa_f.shape[1]
             C = native()
             # gbs = g (s Bbd) [M, k2] (zero past n r): the dgrad tail operand and dA's left factor
-            gbs = C.skinny_xwt(g2, bb_p[:, :nr].t().contiguous(), k2, 1.0)
+            gbs = C.skinny_xwt(g2, bbt, k2, 1.0)
             if ctx.needs_input_grad[0]:
                 dx = C.lora_dgrad(g2, w, gbs, a).view(ctx.xshape)
             if ctx.needs_input_grad[2]:
                 da = C.skinny_ptx(gbs[:, :nr], x2, 1.0)           # (s g Bbd)^T x  [n r, K]
             if any(ctx.needs_input_grad[5:]):
-                full_t = C.skinny_ptx(xa_f[:, :nr], g2, s)        # s xa^T g  [n r, N]
-                r = nr // len(sizes)
-                o = 0
-                for i, n in enumerate(sizes):
-                    dbs[i] = full_t[i * r:(i + 1) * r, o:o + n].t().contiguous()
-                    o += n
+                dbs = _lora_db(xa_f[:, :nr], g2, sizes, s)        # s (xa^T g) diagonal blocks^T
             return (dx, None, da, None, None, g if ctx.has_res else None, *dbs)
         if ctx.fused:
             x2, w, a, xa_f, bb_p = ctx.saved_tensors
@@ -495,21 +489,21 @@ def lora_linear(x: torch.Tensor, w: torch.Tensor, a: torch.Tensor, bs, s: float,
 
 
 def _lora_skinny_operands(x2, a, bs, s):
-    """xa = x A^T ([M, k2], zero past n r) and s Bbd zero-padded to k2 columns."""
-    nr = a.shape[0]
-    k2 = _lora_k2(nr)
+    """xa = x A^T ([M, k2], zero past n r), s Bbd zero-padded to k2 columns and its transpose
+    [n r, N] (skinny.hip: one packing launch instead of block_diag / mul / pad / transpose)."""
+    k2 = _lora_k2(a.shape[0])
     xa = native().skinny_xwt(x2, a, k2, 1.0)
-    bb = a.new_zeros(sum(int(b.shape[0]) for b in bs), k2)
-    torch.mul(torch.block_diag(*bs), s, out=bb[:, :nr])
-    return xa, bb
+    bb, bbt = native().lora_pack_b([b.contiguous() for b in bs], float(s), k2)
+    return xa, bb, bbt
 
 
-def _lora_db(full_t: torch.Tensor, sizes, nr: int):
-    """dB_i from the stacked s xa^T g [n r, N] (block i = rows i r.., columns of output block i)."""
-    r = nr // len(sizes)
+def _lora_db(xa: torch.Tensor, g2: torch.Tensor, sizes, s: float):
+    """The adapters' B gradients dB_i = s (g^T xa)[block i] as contiguous row blocks of ONE
+    [N, r] tensor (the reduce writes the diagonal blocks transposed: no slicing copies)."""
+    full = native().skinny_ptx_bdiag(xa, g2, [int(n) for n in sizes], float(s))
     out, o = [], 0
-    for i, n in enumerate(sizes):
-        out.append(full_t[i * r:(i + 1) * r, o:o + n].t().contiguous())
+    for n in sizes:
+        out.append(full[o:o + n])
         o += n
     return out
 
@@ -535,11 +529,11 @@ class _LoRASwiGLUMLP(torch.autograd.Function):
         bgu, bd = bs[:ngu], bs[ngu:]
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         res2 = res.reshape(-1, wd.shape[0]).contiguous()
-        xa_g, bb_g = _lora_skinny_operands(x2, agu, bgu, sgu)
+        xa_g, bb_g, bbt_g = _lora_skinny_operands(x2, agu, bgu, sgu)
         act, gu = C.lora_fwd_swiglu(x2, wgu, xa_g, bb_g)
-        xa_d, bb_d = _lora_skinny_operands(act, ad, bd, sd)
+        xa_d, bb_d, bbt_d = _lora_skinny_operands(act, ad, bd, sd)
         y = C.lora_fwd(act, wd, xa_d, bb_d, res2)
-        ctx.save_for_backward(x2, wgu, agu, xa_g, bb_g, gu, act, wd, ad, xa_d, bb_d)
+        ctx.save_for_backward(x2, wgu, agu, xa_g, bbt_g, gu, act, wd, ad, xa_d, bbt_d)
         ctx.s = (sgu, sd)
         ctx.sizes = (tuple(int(b.shape[0]) for b in bgu), tuple(int(b.shape[0]) for b in bd))
         ctx.xshape = x.shape
@@ -547,19 +541,19 @@ class _LoRASwiGLUMLP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x2, wgu, agu, xa_g, bb_g, gu, act, wd, ad, xa_d, bb_d = ctx.saved_tensors
+        x2, wgu, agu, xa_g, bbt_g, gu, act, wd, ad, xa_d, bbt_d = ctx.saved_tensors
         (sgu, sd), (zgu, zd) = ctx.s, ctx.sizes
         C = native()
         g2 = gy.reshape(-1, gy.shape[-1]).contiguous()
         nrd, nrg = ad.shape[0], agu.shape[0]
-        gbs_d = C.skinny_xwt(g2, bb_d[:, :nrd].t().contiguous(), xa_d.shape[1], 1.0)
+        gbs_d = C.skinny_xwt(g2, bbt_d, xa_d.shape[1], 1.0)
         dgu = C.lora_dgrad_swiglu(g2, wd, gbs_d, ad, gu)
         dad = C.skinny_ptx(gbs_d[:, :nrd], act, 1.0)
-        dbd = _lora_db(C.skinny_ptx(xa_d[:, :nrd], g2, sd), zd, nrd)
-        gbs_g = C.skinny_xwt(dgu, bb_g[:, :nrg].t().contiguous(), xa_g.shape[1], 1.0)
+        dbd = _lora_db(xa_d[:, :nrd], g2, zd, sd)
+        gbs_g = C.skinny_xwt(dgu, bbt_g, xa_g.shape[1], 1.0)
         dx = C.lora_dgrad(dgu, wgu, gbs_g, agu).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dag = C.skinny_ptx(gbs_g[:, :nrg], x2, 1.0)
-        dbg = _lora_db(C.skinny_ptx(xa_g[:, :nrg], dgu, sgu), zgu, nrg)
+        dbg = _lora_db(xa_g[:, :nrg], dgu, zgu, sgu)
         return (dx, None, dag, None, None, None, dad, None, None, gy, *dbg, *dbd)
 
 

@@ -110,6 +110,24 @@ def _launch_ranks(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _heartbeat(rank: int, what: str, every_s: float = 30.0) -> list:
+    """Rank 0: a daemon thread prints what the bench is doing to stderr every ``every_s`` seconds
+    (a Llama-3-8B federation takes minutes to build and ~15 s per round; the printing never
+    touches the GPU). Returns the mutable status cell."""
+    import threading
+    cell = [what]
+    if rank != 0:
+        return cell
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(every_s)
+            print(f"[bench] {time.time() - t0:.0f}s: {cell[0]}", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+    return cell
+
+
 def _async_mix_desc(fed) -> str:
     g = fed.gossip
     delta = getattr(g, "exchange", "state") == "delta"
@@ -152,10 +170,13 @@ def main():
                         if a.global_test_samples > 0 else {}),
                      **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}),
                      **_overrides(a.set))
+    hb = _heartbeat(rt.rank, "building the federation")
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
+        hb[0] = f"warm-up round {r}"
         fed.run_round(r)
     fed.drain()
+    hb[0] = "timed rounds"
     D.barrier()
     if fed.is_cuda:
         torch.cuda.synchronize()
@@ -202,7 +223,11 @@ def main():
               "lead_wait_s_total": sum(float(h.get("lead_wait_s") or 0.0) for h in timed),
               "torn": sum(float(h.get("torn") or 0.0) for h in timed),
               "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
-              "mixed": sum(float(h.get("mixed") or 0.0) for h in timed)}
+              "mixed": sum(float(h.get("mixed") or 0.0) for h in timed),
+              # this rank's own communication: device time of the comm phase and wire bytes
+              "dev_t_comm_mean_s": dev_mean.get("dev_t_comm", 0.0),
+              "bytes_sent_per_round": (sum(float(h.get("bytes_sent") or 0.0) for h in timed)
+                                       / max(len(timed), 1))}
         multi = {"per_rank": D.all_gather_object(ex)}
     # what one client update weighs on the wire (trainable parameters only: LoRA runs exchange
     # adapters) and what each rank actually sent per timed round (max over ranks)

@@ -14,8 +14,6 @@ d=json.loads([l for l in open('$OUT/$tag.json') if l.startswith('{')][-1])
 pr=d['multi_rank']['per_rank']
 print('$tag', round(d['value'],4), [round(p.get('lead_wait_s_total',0),2) for p in pr], d['final_accuracy'], d['accuracy_curve'], [round(sum(p['stale_rounds'])/len(p['stale_rounds']),2) for p in pr], [round(p['wait_s_total'],2) for p in pr])"
 }
-run n8_delta
-run n8_unbounded --set gossip_max_lead=0
-run n8_same --set drift_same_round_mix=true
+run n8_bounded
 
 true

@@ -1,0 +1,8 @@
+#!/bin/bash
+# LoRA helper kernels' numerics -> config-5 record (learnable signal) + profile; IID protocol + grid
+set -o pipefail
+bash scripts/r4/cfg5.sh || exit 1
+mkdir -p gpurun_out/r4_iidfinal
+timeout -k 10 900 python -u scripts/iid_protocol.py --out gpurun_out/r4_iidfinal/iid_final.json --scratch gpurun_out/r4_iidfinal/tmp.json > gpurun_out/r4_iidfinal/log.txt 2>&1; rc=$?
+grep '^{' gpurun_out/r4_iidfinal/log.txt
+exit $rc

@@ -604,6 +604,31 @@ def test_lora_tail_gemms_match_fp32(M, N, K, nr):
     _close(dx, ref_dx, 5e-2, 2e-2)
 
 
+@pytest.mark.parametrize("sizes,r", [([512, 128, 128], 16), ([768, 768], 16), ([1024], 16), ([256, 64, 64], 8)])
+def test_lora_pack_b_and_block_diagonal_db(sizes, r):
+    """skinny.hip LoRA helpers: lora_pack_b = (s Bbd zero-padded to k2 columns, its [n r, N]
+    transpose) in one launch; skinny_ptx_bdiag = the adapters' dB_i = s (xa^T g)[block i]^T as
+    contiguous row blocks of one [N, r] tensor."""
+    torch.manual_seed(sum(sizes) + r)
+    C = ops.native()
+    N, nr, k2, s = sum(sizes), len(sizes) * r, 128, 2.0
+    bs = [torch.randn(o, r, device=DEV).bfloat16() for o in sizes]
+    bb, bbt = C.lora_pack_b(bs, s, k2)
+    ref = torch.zeros(N, k2, device=DEV)
+    ref[:, :nr] = torch.block_diag(*[b.float() for b in bs]) * s
+    assert torch.equal(bb, ref.bfloat16())
+    assert torch.equal(bbt, ref[:, :nr].t().contiguous().bfloat16())
+    M = 3000
+    xa = torch.randn(M, nr, device=DEV).bfloat16()
+    g = torch.randn(M, N, device=DEV).bfloat16()
+    out = C.skinny_ptx_bdiag(xa, g, sizes, s)
+    full = s * (xa.float().t() @ g.float())
+    o = 0
+    for i, n in enumerate(sizes):
+        _close(out[o:o + n], full[i * r:(i + 1) * r, o:o + n].t(), 2e-2, 2e-2)
+        o += n
+
+
 @pytest.mark.parametrize("M,H,I,nr", [(2048, 512, 768, 32), (8192, 1024, 1536, 32), (1500, 256, 512, 16)])
 def test_lora_swiglu_epilogues_match_fp32(M, H, I, nr):
     """gemm8.hip EPI_SWIGLU: [gate|up] = x Wgu^T + xa bb^T with each output tile pairing gate
