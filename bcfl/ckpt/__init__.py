@@ -129,6 +129,7 @@ class AsyncCheckpointer:
         dev = flat.master.device
         self.cuda = dev.type == "cuda"
         self.pinned: List[torch.Tensor] = []
+        self.snaps: List[torch.Tensor] = []   # device-side snapshots the D2H copies read
         self.stream = torch.cuda.Stream(device=dev) if self.cuda else None
         self.pool = cf.ThreadPoolExecutor(max_workers=1) if async_ else None
         self.future: Optional[cf.Future] = None
@@ -171,14 +172,23 @@ class AsyncCheckpointer:
         jobs = merged
         bufs = [self._buf(i) for i in range(len(jobs))]
         if self.cuda:
+            # snapshot on the device first (one D2D pass at HBM speed on the current stream), then
+            # the D2H copies read the snapshot on the side stream: the training stream never waits
+            # for PCIe (one-client round: the 438 MB D2H was 5.6 ms of device time per round on
+            # the critical path). The next save reuses a snapshot only after this save's writer
+            # thread has synchronised on `done` (busy() -> skipped / waited by the caller).
             cur = torch.cuda.current_stream(self.stream.device)
+            while len(self.snaps) < len(jobs):
+                self.snaps.append(torch.empty(self.flat.numel, dtype=torch.float32,
+                                              device=self.stream.device))
+            for snap, (_, src) in zip(self.snaps, jobs):
+                snap.copy_(src)
             ev = cur.record_event()
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
-                for b, (_, src) in zip(bufs, jobs):
-                    b.copy_(src, non_blocking=True)
+                for b, snap in zip(bufs, self.snaps):
+                    b.copy_(snap, non_blocking=True)
                 done = self.stream.record_event()
-            cur.wait_event(done)  # later writers of the sources are ordered after the copies
         else:
             for b, (_, src) in zip(bufs, jobs):
                 b.copy_(src)

@@ -54,8 +54,10 @@ def build_host(force=False, verbose=False) -> str:
         return out
     inc = sum((["-I", p] for p in _py_includes()), [])
     cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
-           "-Wall", "-Wno-sign-compare", *inc, "-I", os.path.join(HERE, "native"), *srcs, "-o", out]
+           "-Wall", "-Wno-sign-compare", *inc, "-I", os.path.join(HERE, "native"), *srcs, "-o",
+           out + ".tmp"]
     _run(cmd, verbose)
+    os.replace(out + ".tmp", out)
     return out
 
 
@@ -116,10 +118,14 @@ def build_kernels(force=False, verbose=False, jobs=8) -> str:
                 f.result()
     if force or jobs_list or _stale(out, objs):
         lib = sum((["-L", p, f"-Wl,-rpath,{p}"] for p in libdirs), [])
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out, *lib,
+        # link to a temporary file and rename: a reader (an importing process, a tree snapshot)
+        # never sees a half-written library
+        tmp = out + ".tmp"
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, *lib,
                "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
                "-lamdhip64"]
         _run(cmd, verbose)
+        os.replace(tmp, out)
     return out
 
 

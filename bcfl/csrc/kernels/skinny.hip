@@ -22,6 +22,7 @@
 //   reduce:     the slices summed in a fixed order (deterministic), bf16 out, optional zero
 //               columns (the tail-segment padding the fused LoRA GEMMs of gemm8.hip read).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -291,11 +292,20 @@ int launch_lora_pack_b(const LoraPackParams& p, hipStream_t s) {
   return 0;
 }
 
+// grid-size targets (A/B: BCFL_SKINNY_XWT_WAVES, BCFL_SKINNY_PTX_WGS, BCFL_SKINNY_MIN_STEPS)
+static int skinny_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+
 int skinny_xwt_splits(int M, int K, int* kc) {
   // ~2 slices per CU's worth of 32-row waves: at M = 8k, 256 row waves x S slices
+  static const int target = skinny_env("BCFL_SKINNY_XWT_WAVES", 2048);
+  static const int min_steps = skinny_env("BCFL_SKINNY_MIN_STEPS", 8);
   const int waves = (M + 31) / 32;
-  int S = (2048 + waves - 1) / waves;
-  const int maxS = K / 512 > 0 ? K / 512 : 1;  // >= 8 k-steps per slice
+  int S = (target + waves - 1) / waves;
+  const int maxS = K / (64 * min_steps) > 0 ? K / (64 * min_steps) : 1;  // >= min_steps k-steps
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
   int c = (K + S - 1) / S;
@@ -321,8 +331,9 @@ int launch_skinny_xwt(const SkinnyParams& p, hipStream_t s) {
 }
 
 int skinny_ptx_splits(int M, int N, int* mc) {
+  static const int target = skinny_env("BCFL_SKINNY_PTX_WGS", 512);
   const int blocks = N / 64;
-  int S = (512 + blocks - 1) / blocks;
+  int S = (target + blocks - 1) / blocks;
   const int maxS = M / 512 > 0 ? M / 512 : 1;  // >= 16 m-steps per slice
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
