@@ -939,7 +939,10 @@ class Federation:
             allrecs = sorted(allrecs, key=lambda x: (x["client"], x.get("kind", "update"),
                                                      x.get("metrics", {}).get("receiver_rank", -1)))
             for x in allrecs:
-                self.ledger.append(r, x["client"], x.get("kind", "update"), x["root"], x["verdict"],
+                root = x["root"]
+                if not isinstance(root, str):   # a device root tensor (or raw digest bytes)
+                    root = ops.root_bytes(root).hex()
+                self.ledger.append(r, x["client"], x.get("kind", "update"), root, x["verdict"],
                                    x.get("metrics", {}), ts=x["ts"])
             if extra is not None:
                 kind, root = extra.pop("kind", "round"), extra.pop("root", "")
@@ -1211,9 +1214,9 @@ class Federation:
         for g in (take() if take is not None else []):
             if g["kind"] == "update":
                 if g.get("root_t") is not None and g["client"] in by_client and self._gossip_roots:
-                    rt_ = g["root_t"]
-                    by_client[g["client"]]["root"] = rt_ if isinstance(rt_, str) else \
-                        ops.root_bytes(rt_).hex()
+                    # a device tensor stays one until the block is appended (_ledger_round):
+                    # reading it here would wait for the publish hash
+                    by_client[g["client"]]["root"] = g["root_t"]
                 if g["client"] in by_client:
                     by_client[g["client"]].setdefault("metrics", {})["version"] = g["version"]
             elif g["kind"] == "recv":
@@ -1249,6 +1252,8 @@ class Federation:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
         need_prev = self.filter is not None or bool(cfg.inject_byzantine)
+        self._run_deferred()            # last round's host reads (its kernels have finished)
+        self._resolve_eval_local()      # last round's deferred local scores (long finished)
         lead_wait = self._bound_lead(r)
         if self.outer.enabled:
             for c in self.local_clients:
@@ -1275,7 +1280,10 @@ class Federation:
             losses[c] = st
             if cfg.eval_local:
                 with self.timer.phase("eval_local"):
-                    local_eval[c] = self.trainer.evaluate_device(self.test_batches(c, r))
+                    if self._defer_local_eval():
+                        self._launch_eval_local(c, r)
+                    else:
+                        local_eval[c] = self.trainer.evaluate_device(self.test_batches(c, r))
             root = self._merkle() if self.ledger is not None and not self._gossip_roots else ""
             recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
                          "verdict": "accept", "metrics": {"examples": st["examples"]}})
@@ -1326,10 +1334,20 @@ class Federation:
         if self.verbose and cfg.reference_prints:
             for c, _, m in sorted(client_metrics):
                 print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
-        train_loss = self._reduce_train_loss(losses)
-        self._ledger_round(r, recs, {"kind": "mix", "rejected": sorted(v.rejected),
-                                     "stale_rounds": info.get("stale_rounds", 0.0),
-                                     "dead_peers": sorted(self.gossip.dead)})
+        ledger_extra = {"kind": "mix", "rejected": sorted(v.rejected),
+                        "stale_rounds": info.get("stale_rounds", 0.0),
+                        "dead_peers": sorted(self.gossip.dead)}
+        if self.collective_free and self.is_cuda:
+            # nothing of this round is read back on the host now (the loss sum and the ledger's
+            # Merkle roots wait for the round's last kernels): the next round's work is queued
+            # while this round's tail still runs, and the reads happen at its start
+            train_loss = None
+            self._defer(lambda r=r, losses=losses: self._patch_history(
+                r, train_loss=self._reduce_train_loss(losses)))
+            self._defer(lambda r=r, recs=recs, ex=ledger_extra: self._ledger_round(r, recs, ex))
+        else:
+            train_loss = self._reduce_train_loss(losses)
+            self._ledger_round(r, recs, ledger_extra)
         agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
         return {"distributed_accuracy": agg.get("accuracy"), "distributed_loss": agg.get("loss"),
                 "global": ge, "train_loss": train_loss, "rejected": sorted(v.rejected),
@@ -1339,6 +1357,87 @@ class Federation:
                 "wait_s": info.get("wait_s", 0.0) + lead_wait, "lead_wait_s": lead_wait,
                 "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
                 "rejected_msgs": info.get("rejected_msgs", 0.0)}
+
+    # ---- host reads deferred to the next round --------------------------------------------------
+    def _defer(self, fn) -> None:
+        if not hasattr(self, "_deferred"):
+            self._deferred = []
+        self._deferred.append(fn)
+
+    def _run_deferred(self) -> None:
+        fns, self._deferred = getattr(self, "_deferred", []), []
+        for fn in fns:
+            fn()
+
+    def _patch_history(self, r: int, **kw) -> None:
+        for rec in reversed(self.history):
+            if rec.get("round") == r:
+                rec.update(kw)
+                break
+        self.metrics.write({"round": r, "deferred": True, **kw})
+
+    # ---- local evaluation off the critical path (one client trained at a time) ----------------
+    def _defer_local_eval(self) -> bool:
+        """A rank that trains its clients one at a time (the 8-GPU layout: one client per GPU)
+        scores the trained model on its local test rows on the eval side stream, from a snapshot,
+        while gossip and the next round run (collective-free federations only: the metrics are
+        filed when the host reads them, the next round)."""
+        return (self.eval_stream is not None and self.collective_free and not self.lanes
+                and self.cfg.eval_local and not self.cfg.compat_chain)
+
+    def _launch_eval_local(self, c: int, r: int) -> None:
+        main = torch.cuda.current_stream(self.device)
+        if not hasattr(self, "_local_snaps"):
+            self._local_snaps = [torch.empty_like(self.flat.param) for _ in range(2)]
+            self._local_done: List[Optional[torch.cuda.Event]] = [None, None]
+            self._local_pending: List[tuple] = []
+            self._local_k = 0
+        i = self._local_k % 2
+        self._local_k += 1
+        if self._local_done[i] is not None:
+            main.wait_event(self._local_done[i])   # the evaluation that last read this snapshot
+        snap = self._local_snaps[i]
+        snap.copy_(self.flat.param)                # the trained model, before the mix
+        batches = self.test_batches(c, r)          # uploaded on the training stream
+        es = self.eval_stream
+        es.wait_stream(main)
+        own = self.eval_flat.param
+        with torch.cuda.stream(es):
+            self.eval_flat.rebind(self.eval_flat.master, snap)
+            stats = self.eval_trainer.evaluate_device(batches)
+            ev = torch.cuda.Event()
+            ev.record(es)
+        # the queued kernels hold the snapshot's pointers; the replica's own buffer is what the
+        # global evaluation copies into (no later reader of the snapshot but this evaluation)
+        self.eval_flat.rebind(self.eval_flat.master, own)
+        self._local_done[i] = ev
+        # the batches stay referenced until the statistics are read (their memory belongs to
+        # the training stream's pool)
+        self._local_pending.append((r, c, stats, ev, batches))
+
+    def _resolve_eval_local(self) -> None:
+        pend = getattr(self, "_local_pending", None)
+        if not pend:
+            return
+        self._local_pending = []
+        by_round: Dict[int, list] = {}
+        for r, c, stats, ev, _b in pend:
+            ev.synchronize()
+            a = stats.cpu().tolist()
+            e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+            m = {"accuracy": e.accuracy, "loss": e.ref_loss if self.cfg.compat_bad_test_loss else e.loss}
+            by_round.setdefault(r, []).append((c, e.count, m))
+            if self.verbose and self.cfg.reference_prints:
+                print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
+            self.metrics.write({"round": r, "client": c, "local_acc": m.get("accuracy"),
+                                "local_loss": m.get("loss"), "examples": e.count,
+                                "deferred_local_eval": True})
+        for r, cm in by_round.items():
+            agg = weighted_average([(n_, m) for _, n_, m in cm])
+            for rec in reversed(self.history):
+                if rec.get("round") == r:
+                    rec["distributed_acc"] = agg.get("accuracy")
+                    break
 
     def _chain_round(self, r: int) -> dict:
         """Reference C14 exactly: clients train one after another on ONE shared model; the
@@ -1434,6 +1533,8 @@ class Federation:
             self._resolve_eval()
         if self.ckpt is None:
             return
+        if cfg.save_resume_state:
+            self._run_deferred()   # the resume state must carry this round's ledger tip
         if self.ckpt.busy():
             if cfg.save_resume_state:
                 # resumable runs never skip: every rank's files of a save belong to ONE round
@@ -1519,6 +1620,8 @@ class Federation:
     def drain(self):
         """Complete all in-flight communication (async gossip), evaluation and I/O."""
         self._resolve_eval()
+        self._run_deferred()
+        self._resolve_eval_local()
         if self.gossip is not None:
             self.gossip.drain()
         if self.server_mbox is not None:

@@ -137,6 +137,36 @@ def test_gpu_overlapped_global_eval_matches_inline(tmp_path, mode):
     assert float((a_m - b_m).abs().max()) < 2e-4
 
 
+def test_gpu_deferred_local_eval_matches_inline(tmp_path):
+    """One client per rank (the 8-GPU layout): the local evaluation of the trained model runs on
+    the eval side stream from a snapshot and is filed the next round; the scores, the metrics
+    lines and the training it overlaps equal the inline path's."""
+    import json
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    outs = []
+    for ov in (False, True):
+        D.set_runtime_for_tests(None)
+        out = str(tmp_path / str(ov))
+        cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=1,
+                       num_rounds=3, train_samples=64, test_samples=32, global_test_samples=64,
+                       out_dir=out, reference_prints=False, save_every=0, overlap_wgrad=False,
+                       dropout=0.1, async_gossip=True, gossip_transport="mailbox",
+                       overlap_global_eval=ov, eval_local=True)
+        fed = Federation(cfg, verbose=False)
+        assert fed._defer_local_eval() == ov
+        h = fed.run()
+        loc = [json.loads(l) for l in open(os.path.join(out, "metrics.jsonl")) if '"local_acc"' in l]
+        outs.append(([r["distributed_acc"] for r in h], [(x["round"], x["local_acc"]) for x in loc],
+                     fed.flat.master.detach().cpu()))
+        D.set_runtime_for_tests(None)
+    (a_d, a_l, a_m), (b_d, b_l, b_m) = outs
+    assert None not in b_d and b_d == a_d
+    assert sorted(b_l) == sorted(a_l)
+    assert float((a_m - b_m).abs().max()) < 2e-4
+
+
 def test_gpu_micro_batch_clients_match_full_batch(tmp_path):
     """Server mode trains one client at a time: with micro_batches=2 (2 concurrent micro-batches
     on 2 streams) the run tracks the full-batch run (dropout off; bf16 gradient sums round

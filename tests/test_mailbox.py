@@ -211,7 +211,8 @@ def test_mailbox_async_two_ranks_slow_peer_learn_label_shards(tmp_path):
     post (stale-exact c_hat). The round-3 alternative (state mixing of stale snapshots, mix-derived
     c') stayed near the majority rate (0.50 on MI355X, profiles/multirank_learning_r3.json)."""
     res = run_world(_learn_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"inject_slow": {1: 200.0}, "liveness_timeout": 6, "gossip_max_lead": 0})
+                    {"inject_slow": {1: 200.0}, "liveness_timeout": 6, "gossip_max_lead": 0,
+                     "num_rounds": 20})
     _check_async_learning(res)
 
 
