@@ -61,6 +61,8 @@ class FLConfig:
     adam_eps: float = 1e-6
     adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
     keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
+    async_keep_optimizer_state: bool = True  # ... except under asynchronous delta-exchange
+    #                                     gossip, where each client keeps its AdamW moments
     max_grad_norm: float = 0.0          # global-norm gradient clipping per local step (0 = off:
                                         # the reference's plain loop); fused into the AdamW pass
     drift_correction: str = "none"      # none | scaffold | auto (control variates in update
@@ -115,6 +117,10 @@ class FLConfig:
                                         # sum; a rank that stops posting is left out and the weights
                                         # re-normalised over the live ranks — Flower accept_failures)
     server_timeout_s: float = 120.0     # mailbox server: how long a round waits for a rank's post
+    overlap_optimizer: Optional[bool] = None  # one-lane GPU ranks: per-layer AdamW on a side
+    #                                     stream launched from the gradient hooks mid-backward
+    #                                     (None = with the side-stream weight gradients, no
+    #                                     clipping / micro-batches / deterministic mode)
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
     micro_batches: int = 0              # a rank training ONE client at a time splits each batch into

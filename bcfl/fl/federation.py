@@ -172,6 +172,11 @@ class Federation:
         if cfg.deterministic:
             ov = False  # the overlapped path's gradients are not bitwise reproducible
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
+        oo = cfg.overlap_optimizer
+        if oo is None:
+            oo = bool(ov) and self.is_cuda and cfg.max_grad_norm <= 0 and not cfg.deterministic
+        if oo and self.is_cuda and len(self.lanes) <= 1 and self.micro_split == 1:
+            self.opt.enable_overlap()
         if self.is_cuda and ops.native_available():
             # persistent GEMM grids (one workgroup per CU walking the tiles) pay with concurrent
             # client lanes (8-lane round 0.5635 -> 0.5604 s, profiles/g8_persistent_r3.json) and
@@ -280,6 +285,16 @@ class Federation:
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
             self.gossip.tamper = set(cfg.inject_tamper) & set(self.local_clients)
             self.gossip.seed_replicas(self.flat.master)
+        # the clients' AdamW moments persist across rounds when asked for, and under asynchronous
+        # delta exchange: a fresh AdamW per fit (the reference, C8) takes sign-like first steps
+        # every round, and with 8 ranks mixing stale updates the federation then stays on the
+        # plateau (CPU, 8 ranks, lr 5e-4: 0.50 fresh vs 0.995 kept, 2 / 2 runs each; one process:
+        # the same either way)
+        self.keep_opt = bool(cfg.keep_optimizer_state or (
+            cfg.async_keep_optimizer_state and isinstance(self.gossip, MailboxGossip)
+            and self.gossip.exchange == "delta"))
+        self._single_opt = not self.multi   # one client, one optimizer: keep it in place
+        self._opt_owner: Optional[int] = None
         # ---------------- trust ---------------------------------------------------------------------
         self.filter = UpdateAnomalyFilter(cfg.anomaly_filter, cfg.anomaly_k,
                                           cfg.anomaly_modz_threshold) if cfg.anomaly_filter != "none" else None
@@ -480,7 +495,7 @@ class Federation:
         for c in lane.clients:
             with self._on(lane):
                 lane.flat.rebind(self.client_master[c], self.client_param[c])
-                if cfg.keep_optimizer_state and c in self.client_opt:
+                if self.keep_opt and c in self.client_opt:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
@@ -523,7 +538,7 @@ class Federation:
                     out["local_eval"][c] = lane.trainer.evaluate_device(self.test_batches(c, r))
                 out["roots"][c] = (ops.merkle_root_deferred(lane.flat.master)
                                    if self.ledger is not None and not self._gossip_roots else None)
-                if cfg.keep_optimizer_state:
+                if self.keep_opt:
                     self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
                                           for k, v in lane.opt.state_dict().items()}
             yield
@@ -560,7 +575,7 @@ class Federation:
         for c in lane.clients:
             with self._on(lane):
                 lane.flat.load_master(G)
-                if cfg.keep_optimizer_state and c in self.client_opt:
+                if self.keep_opt and c in self.client_opt:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
@@ -595,7 +610,7 @@ class Federation:
                     out["trained"][c] = lane.flat.master.detach().clone()
                 else:
                     ops.weighted_accumulate_(acc, lane.flat.master, float(w[c]))
-                if cfg.keep_optimizer_state:
+                if self.keep_opt:
                     self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
                                           for k, v in lane.opt.state_dict().items()}
             yield
@@ -860,10 +875,12 @@ class Federation:
             self.flat.load_master(master)
         elif self.multi and c in self.client_master:
             self.flat.load_master(self.client_master[c])
-        if self.cfg.keep_optimizer_state and c in self.client_opt:
-            self.opt.load_state_dict(self.client_opt[c])
-        else:
+        if self.keep_opt and c in self.client_opt:
+            self.opt.load_state_dict(self.client_opt.pop(c) if self._single_opt else self.client_opt[c])
+            self._opt_owner = c
+        elif not (self.keep_opt and self._single_opt and self._opt_owner == c):
             self.opt.reset()
+            self._opt_owner = c
         self.drift.attach(self.opt, c, self.flat.master)
         self._mark_start(c, self.flat.master)
         ops.rng.global_rng().load_state(self.client_rng[c])
@@ -871,7 +888,7 @@ class Federation:
     def _deactivate(self, c: int):
         if self.multi and c in self.client_master:
             self.client_master[c].copy_(self.flat.master)
-        if self.cfg.keep_optimizer_state:
+        if self.keep_opt and not self._single_opt:
             self.client_opt[c] = {k: (v.clone() if torch.is_tensor(v) else v)
                                   for k, v in self.opt.state_dict().items()}
         self.client_rng[c] = ops.rng.global_rng().state()
@@ -1577,6 +1594,13 @@ class Federation:
                                state=state if self.rt.is_main else None, jobs=jobs,
                                extra_files=extra)
 
+    def _opt_states(self) -> Dict[int, dict]:
+        """Kept optimizer states per client (a one-client rank keeps its live optimizer)."""
+        st = dict(self.client_opt)
+        if self.keep_opt and self._single_opt and self._opt_owner is not None:
+            st[self._opt_owner] = self.opt.state_dict()
+        return st
+
     def resume_state(self, r: int) -> dict:
         """Per-rank training state (tensors on the host; loadable with ``weights_only=True``)."""
         cpu = lambda t: t.detach().cpu().clone()  # noqa: E731
@@ -1586,7 +1610,7 @@ class Federation:
               "client_master": {int(c): cpu(t) for c, t in self.client_master.items()},
               "master": cpu(self.flat.master),
               "client_opt": {int(c): {"m": cpu(o["m"]), "v": cpu(o["v"]), "step": int(o["step"])}
-                             for c, o in self.client_opt.items()},
+                             for c, o in self._opt_states().items()},
               "prev_rejected": sorted(self.prev_verdicts.rejected),
               "drift": self.drift.state_dict(),
               "outer": self.outer.state_dict(),

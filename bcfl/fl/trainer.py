@@ -95,10 +95,17 @@ class LocalTrainer:
         self.model.train()
         logits = self.model(b)
         loss = ops.cross_entropy(logits, b.labels)
-        loss.backward()
-        if self.flat.device.type == "cuda":
-            ops.join_wgrad(self.flat.device)  # overlapped weight gradients -> optimizer
-        self.opt.step()
+        if self.opt.overlap_active():
+            # per-layer AdamW on a side stream, launched from the gradient hooks mid-backward
+            self.opt.begin_overlapped()
+            loss.backward()
+            ops.join_wgrad(self.flat.device)
+            self.opt.finish_overlapped()
+        else:
+            loss.backward()
+            if self.flat.device.type == "cuda":
+                ops.join_wgrad(self.flat.device)  # overlapped weight gradients -> optimizer
+            self.opt.step()
         self.flat.zero_grad()
         loss_acc += loss.detach()
 

@@ -175,6 +175,92 @@ class FlatAdamW:
                          grad_scale=grad_scale, corr=self.corr,
                          corr_lr=self.lr * self.corr_scale, grads2=grads2, gscale=gscale)
 
+    # ---- optimizer overlapped with the backward pass ---------------------------------------
+    # A rank that trains ONE client (the 8-GPU layout) runs its AdamW pass after the last
+    # gradient of the step otherwise (~0.7 ms of HBM-bound work per BERT-base step on the
+    # critical path). With overlap, each layer's parameters are updated on a side stream as soon
+    # as autograd has produced the layer's last gradient, while the backward pass continues
+    # through the earlier layers (which never read the later layers' weights). The update is the
+    # same element-wise AdamW, so results are bitwise those of step().
+    @staticmethod
+    def _group_key(name: str) -> str:
+        parts = name.split(".")
+        for i, t in enumerate(parts[:-1]):
+            if t in ("layer", "layers") and parts[i + 1].isdigit():
+                return ".".join(parts[:i + 2])
+        return parts[0]
+
+    def enable_overlap(self) -> bool:
+        f = self.flat
+        if f.device.type != "cuda" or getattr(self, "overlap", False):
+            return getattr(self, "overlap", False)
+        keys = [self._group_key(n) for n in f.names]
+        self._groups, self._gid = [], []
+        for i, k in enumerate(keys):
+            if i == 0 or keys[i - 1] != k:
+                self._groups.append([])
+            self._groups[-1].append(i)
+            self._gid.append(len(self._groups) - 1)
+        self._astream = torch.cuda.Stream(device=f.device)
+        self._live = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
+                       for i, p in enumerate(f.params)]
+        self.overlap = True
+        return True
+
+    def overlap_active(self) -> bool:
+        return getattr(self, "overlap", False) and self.max_grad_norm <= 0
+
+    def _hook(self, i: int):
+        def fn(_p):
+            if self._live:
+                g = self._gid[i]
+                self._left[g] -= 1
+                if self._left[g] == 0:
+                    self._launch(g)
+        return fn
+
+    def begin_overlapped(self, grad_scale: float = 1.0) -> None:
+        """Before backward(): open the step (groups launch from the gradient hooks)."""
+        self.step_count += 1
+        self._left = [len(g) for g in self._groups]
+        self._launched = [False] * len(self._groups)
+        self._main = torch.cuda.current_stream(self.flat.device)
+        self._gs = grad_scale
+        self._live = True
+
+    @torch.no_grad()
+    def _launch(self, g: int) -> None:
+        from ..ops import functional as _F
+        self._launched[g] = True
+        f = self.flat
+        idx = [i for i in self._groups[g] if f.params[i].grad is not None]
+        if not idx:
+            return
+        grads = [f.params[i].grad for i in idx]
+        offs = [f.slots[i][0] for i in idx]
+        a, main = self._astream, self._main
+        a.wait_stream(main)
+        side = _F._WG["side"].get((main.device_index, main.cuda_stream))
+        if side is not None:   # side-stream weight gradients launched from this stream
+            a.wait_stream(side)
+        with torch.cuda.stream(a):
+            for t in grads:
+                t.record_stream(a)
+            ops.adamw_multi_(f.master, grads, offs, self.m, self.v, self.step_count, self.lr,
+                             self.betas[0], self.betas[1], self.eps, self.wd, self.mode,
+                             param_out=None if f.master is f.param else f.param,
+                             grad_scale=self._gs, corr=self.corr,
+                             corr_lr=self.lr * self.corr_scale)
+
+    def finish_overlapped(self) -> None:
+        """After backward(): update what no hook launched, then the step's stream waits."""
+        self._live = False
+        for g in range(len(self._groups)):
+            if not self._launched[g]:
+                self._launch(g)
+        self._main.wait_stream(self._astream)
+
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}
 

@@ -285,7 +285,7 @@ def main():
             "accuracy_note": ACCURACY_NOTE,
             "accuracy_protocol": {"lr": cfg.lr, "lr_schedule": cfg.lr_schedule,
                                   "lr_warmup_steps": cfg.lr_warmup_steps,
-                                  "keep_optimizer_state": cfg.keep_optimizer_state,
+                                  "keep_optimizer_state": bool(getattr(fed, "keep_opt", cfg.keep_optimizer_state)),
                                   "synthetic_signal": cfg.synthetic_signal,
                                   "drift_correction": fed.drift.mode,
                                   "rounds_trained": a.warmup + a.steps},

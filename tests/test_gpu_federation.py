@@ -167,6 +167,31 @@ def test_gpu_deferred_local_eval_matches_inline(tmp_path):
     assert float((a_m - b_m).abs().max()) < 2e-4
 
 
+@pytest.mark.parametrize("drift", ["none", "scaffold"])
+def test_gpu_overlapped_optimizer_is_bitwise(tmp_path, drift):
+    """Per-layer AdamW launched from the gradient hooks on a side stream mid-backward (one-lane
+    ranks) gives bitwise the same models as the one-pass AdamW after the backward."""
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    outs = []
+    for oo in (False, True):
+        D.set_runtime_for_tests(None)
+        cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=1,
+                       num_rounds=2, train_samples=96, test_samples=32, global_test_samples=64,
+                       out_dir=str(tmp_path / f"{oo}"), reference_prints=False, save_every=0,
+                       dropout=0.1, overlap_wgrad=True, overlap_optimizer=oo,
+                       drift_correction=drift)
+        fed = Federation(cfg, verbose=False)
+        assert fed.opt.overlap_active() == oo
+        h = fed.run()
+        outs.append((fed.flat.master.detach().cpu(), fed.flat.param.detach().cpu(),
+                     [r["train_loss"] for r in h]))
+        D.set_runtime_for_tests(None)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+
+
 def test_gpu_micro_batch_clients_match_full_batch(tmp_path):
     """Server mode trains one client at a time: with micro_batches=2 (2 concurrent micro-batches
     on 2 streams) the run tracks the full-batch run (dropout off; bf16 gradient sums round
