@@ -117,10 +117,9 @@ class FLConfig:
                                         # sum; a rank that stops posting is left out and the weights
                                         # re-normalised over the live ranks — Flower accept_failures)
     server_timeout_s: float = 120.0     # mailbox server: how long a round waits for a rank's post
-    overlap_optimizer: Optional[bool] = None  # one-lane GPU ranks: per-layer AdamW on a side
-    #                                     stream launched from the gradient hooks mid-backward
-    #                                     (None = with the side-stream weight gradients, no
-    #                                     clipping / micro-batches / deterministic mode)
+    overlap_optimizer: bool = False     # one-lane GPU ranks: per-layer AdamW on a side stream
+    #                                     launched from the gradient hooks mid-backward (bitwise;
+    #                                     measured slower on BERT-base, so off by default)
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
     micro_batches: int = 0              # a rank training ONE client at a time splits each batch into

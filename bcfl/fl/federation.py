@@ -172,9 +172,10 @@ class Federation:
         if cfg.deterministic:
             ov = False  # the overlapped path's gradients are not bitwise reproducible
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
-        oo = cfg.overlap_optimizer
-        if oo is None:
-            oo = bool(ov) and self.is_cuda and cfg.max_grad_norm <= 0 and not cfg.deterministic
+        # off by default: measured slower on the one-client round (0.0946 vs 0.0928 s/round,
+        # profiles/bench_r4_1client_*.json) — the side-stream AdamW competes with the backward
+        # GEMMs for HBM and the hooks add host work on the autograd thread
+        oo = bool(cfg.overlap_optimizer) and cfg.max_grad_norm <= 0 and not cfg.deterministic
         if oo and self.is_cuda and len(self.lanes) <= 1 and self.micro_split == 1:
             self.opt.enable_overlap()
         if self.is_cuda and ops.native_available():
