@@ -477,7 +477,8 @@ class Federation:
                     nw = g.transport.newest(h)
                     if nw is not None:
                         posted[j] = nw[1].round
-            time.sleep(0.0005)
+            # every poll queues header reads on the GPU: a few hundred per second, not thousands
+            time.sleep(0.003)
         return time.perf_counter() - t0
 
     @contextlib.contextmanager
@@ -1355,10 +1356,13 @@ class Federation:
         ledger_extra = {"kind": "mix", "rejected": sorted(v.rejected),
                         "stale_rounds": info.get("stale_rounds", 0.0),
                         "dead_peers": sorted(self.gossip.dead)}
-        if self.collective_free and self.is_cuda:
+        if self.collective_free and self.is_cuda and not self.rt.distributed:
             # nothing of this round is read back on the host now (the loss sum and the ledger's
             # Merkle roots wait for the round's last kernels): the next round's work is queued
-            # while this round's tail still runs, and the reads happen at its start
+            # while this round's tail still runs, and the reads happen at its start. Multi-rank
+            # runs keep the round-end read: it paces the host to its GPU, so the bounded-lead
+            # check compares rounds the device has actually finished (deferred, 8 ranks sharing
+            # one GPU spent ~0.8 s per round in lead waits and ran 3x slower)
             train_loss = None
             self._defer(lambda r=r, losses=losses: self._patch_history(
                 r, train_loss=self._reduce_train_loss(losses)))

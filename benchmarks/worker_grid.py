@@ -86,8 +86,13 @@ def main(argv=None):
                          "init, profiles/accuracy_server_stability.json); default keeps moments")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra FLConfig override (JSON value), e.g. --set max_grad_norm=1.0")
+    ap.add_argument("--protocol", choices=["iid", "none"], default="iid",
+                    help="iid: the IID learning protocol (bcfl.config.IID_PROTOCOL) under the "
+                         "--set overrides; none: baseline3_learnable's label-shard settings")
     a = ap.parse_args(argv)
-    extra = {}
+    from bcfl.config import IID_PROTOCOL
+    extra = dict(IID_PROTOCOL) if a.protocol == "iid" else {}
+    extra.pop("keep_optimizer_state", None)   # governed by --fresh-adamw
     for it in a.set:
         k, _, v = it.partition("=")
         try:

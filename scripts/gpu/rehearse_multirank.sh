@@ -1,0 +1,20 @@
+#!/bin/bash
+# N ranks as processes sharing ONE GPU (gloo collectives, hipIpc mailboxes): the bench's multi-rank
+# path with accuracy, staleness and wait statistics per rank.
+#   bash scripts/gpu/rehearse_multirank.sh N TAG [extra bench.py args, e.g. --set gossip_max_lead=0]
+set -o pipefail
+N=${1:?ranks}; TAG=${2:?tag}; shift 2
+OUT=${OUT:-gpurun_out/multirank}
+mkdir -p $OUT
+export BCFL_DIST_BACKEND=gloo
+timeout -k 10 450 python -u bench.py --gpus $N --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-info-passing "$@" \
+  > $OUT/$TAG.json 2> $OUT/$TAG.err || { echo "$TAG rc=$?"; tail -20 $OUT/$TAG.err; exit 1; }
+python3 - $OUT/$TAG.json $TAG <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+pr = d.get("multi_rank", {}).get("per_rank", [])
+print(sys.argv[2], "s/round", round(d["value"], 4), "final", d["final_accuracy"], "curve", d["accuracy_curve"])
+print("  stale mean", [round(sum(p["stale_rounds"]) / max(1, len(p["stale_rounds"])), 2) for p in pr],
+      "wait s", [round(p["wait_s_total"], 2) for p in pr], "lead wait s",
+      [round(p.get("lead_wait_s_total", 0), 2) for p in pr])
+PY
