@@ -148,6 +148,51 @@ __global__ __launch_bounds__(EW_THREADS) void rope_kernel(const T* __restrict__ 
   }
 }
 
+// bf16, 16-byte vectors: one thread rotates 8 consecutive pairs (x[j], x[j + d/2]) of one head
+// (cos / sin as two float4 loads each from the table row of the token's position) or copies 8
+// elements of the non-rotated tail (v); ~5x less time than the element-pair kernel at the
+// Llama-3-8B qkv shape ([8k, 6144], profiles/config5_kernel_stats_r4.md: 163 us per call)
+__global__ __launch_bounds__(EW_THREADS) void rope_vec_kernel(const bf16_t* __restrict__ x,
+                                                             bf16_t* __restrict__ out,
+                                                             const int* __restrict__ pos,
+                                                             const float* __restrict__ cosb,
+                                                             const float* __restrict__ sinb,
+                                                             int64_t rows, int stride, int nrot,
+                                                             int d, int inverse) {
+  const int half = d / 2, hv = half / 8;
+  const int rot_v = nrot * hv, cp_v = (stride - nrot * d) / 8;
+  const int per_row = rot_v + cp_v;
+  const int64_t total = rows * per_row;
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    const int64_t r = i / per_row;
+    const int w = (int)(i - r * per_row);
+    const int64_t rb = r * stride;
+    if (w < rot_v) {
+      const int h = w / hv, j0 = (w - h * hv) * 8;
+      const int64_t t = (int64_t)pos[r] * half + j0;
+      float c[8], sn[8], x1[8], x2[8], y1[8], y2[8];
+      Vec8<float>::load(cosb + t, c);
+      Vec8<float>::load(sinb + t, sn);
+      const int64_t a = rb + (int64_t)h * d + j0;
+      Vec8<bf16_t>::load(x + a, x1);
+      Vec8<bf16_t>::load(x + a + half, x2);
+      const float sg = inverse ? -1.f : 1.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float se = sg * sn[e];
+        y1[e] = x1[e] * c[e] - x2[e] * se;
+        y2[e] = x2[e] * c[e] + x1[e] * se;
+      }
+      Vec8<bf16_t>::store(out + a, y1);
+      Vec8<bf16_t>::store(out + a + half, y2);
+    } else {
+      const int64_t a = rb + (int64_t)nrot * d + 8 * (w - rot_v);
+      *reinterpret_cast<uint4*>(out + a) = *reinterpret_cast<const uint4*>(x + a);
+    }
+  }
+}
+
 template <typename TD, typename TS>
 __global__ __launch_bounds__(EW_THREADS) void cast_kernel(TD* __restrict__ dst,
                                                          const TS* __restrict__ src, int64_t n) {
@@ -549,6 +594,15 @@ int launch_rope(const void* x, void* out, const int* pos, const float* cos, cons
                 int64_t rows, int row_stride, int nrot, int d, int inverse, int dt, hipStream_t s) {
   if (row_stride % 2 || d % 2 || nrot * d > row_stride) return -2;
   const int64_t total = rows * (row_stride / 2);
+  const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0) &&
+                       ((uintptr_t)cos % 16 == 0) && ((uintptr_t)sin % 16 == 0);
+  if (dt == DT_BF16 && d % 16 == 0 && row_stride % 8 == 0 && aligned) {
+    const int64_t tv = rows * (nrot * (d / 16) + (row_stride - nrot * d) / 8);
+    hipLaunchKernelGGL(rope_vec_kernel, dim3(ew_grid(tv)), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)x, (bf16_t*)out, pos, cos, sin, rows, row_stride, nrot, d,
+                       inverse);
+    return 0;
+  }
   if (dt == DT_BF16)
     hipLaunchKernelGGL(rope_kernel<bf16_t>, dim3(ew_grid(total)), dim3(EW_THREADS), 0, s,
                        (const bf16_t*)x, (bf16_t*)out, pos, cos, sin, rows, row_stride, nrot, d, inverse);

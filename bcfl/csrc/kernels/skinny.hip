@@ -331,7 +331,7 @@ int launch_skinny_xwt(const SkinnyParams& p, hipStream_t s) {
 }
 
 int skinny_ptx_splits(int M, int N, int* mc) {
-  static const int target = skinny_env("BCFL_SKINNY_PTX_WGS", 512);
+  static const int target = skinny_env("BCFL_SKINNY_PTX_WGS", 1024);  // sweep: 512 470 us, 1024 425 us over the config-5 shapes (profiles/skinny_sweep_r4.txt)
   const int blocks = N / 64;
   int S = (target + blocks - 1) / blocks;
   const int maxS = M / 512 > 0 ? M / 512 : 1;  // >= 16 m-steps per slice

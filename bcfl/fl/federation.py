@@ -1521,7 +1521,7 @@ class Federation:
                "distributed_acc": res.get("distributed_accuracy"), "train_loss": res.get("train_loss"),
                "rejected": res.get("rejected"), "bytes_sent": res.get("bytes_sent"),
                "dead_peers": res.get("dead_peers", []),
-               **{k: res[k] for k in ("mixed", "stale_rounds", "stale_max", "wait_s", "torn",
+               **{k: res[k] for k in ("mixed", "stale_rounds", "stale_max", "wait_s", "lead_wait_s", "torn",
                                       "rejected_msgs", "absent_ranks", "live_weight",
                                       "view_mismatch", "rejoined_ranks") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
