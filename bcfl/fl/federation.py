@@ -1404,8 +1404,12 @@ class Federation:
         scores the trained model on its local test rows on the eval side stream, from a snapshot,
         while gossip and the next round run (collective-free federations only: the metrics are
         filed when the host reads them, the next round)."""
+        # single-process runs only: with several processes time-slicing one GPU (the multi-rank
+        # rehearsal) the extra side-stream work per rank slowed rounds and stretched the ranks'
+        # lead waits
         return (self.eval_stream is not None and self.collective_free and not self.lanes
-                and self.cfg.eval_local and not self.cfg.compat_chain)
+                and self.cfg.eval_local and not self.cfg.compat_chain
+                and not self.rt.distributed)
 
     def _launch_eval_local(self, c: int, r: int) -> None:
         main = torch.cuda.current_stream(self.device)

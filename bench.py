@@ -139,6 +139,8 @@ def _async_mix_desc(fed) -> str:
           if lead > 0 and fed.rt.distributed else "; never waits")
     if fed.drift.exchange:
         d += " + exchanged SCAFFOLD control variates (stale-exact)"
+    if delta and getattr(fed, "keep_opt", False) and not fed.cfg.keep_optimizer_state:
+        d += "; client AdamW moments kept across rounds"
     return d
 
 
