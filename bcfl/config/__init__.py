@@ -61,8 +61,12 @@ class FLConfig:
     adam_eps: float = 1e-6
     adam_mode: str = "hf"               # "hf" (transformers.AdamW 4.35) | "torch" (torch.optim.AdamW)
     keep_optimizer_state: bool = False  # reference recreates AdamW every fit (C8)
-    async_keep_optimizer_state: bool = True  # ... except under asynchronous delta-exchange
-    #                                     gossip, where each client keeps its AdamW moments
+    async_keep_optimizer_state: bool = False  # asynchronous delta-exchange gossip: keep each
+    #                                     client's AdamW moments across rounds. Off: on MI355X at
+    #                                     the bench config (BERT-base, lr 2e-5, 4 ranks) fresh
+    #                                     AdamW learns (0.904 / 0.959) and kept moments do not
+    #                                     (0.669 / 0.50); the CPU tiny-bert 8-rank case at lr 5e-4
+    #                                     is the opposite (profiles/multirank_async_r4.json)
     max_grad_norm: float = 0.0          # global-norm gradient clipping per local step (0 = off:
                                         # the reference's plain loop); fused into the AdamW pass
     drift_correction: str = "none"      # none | scaffold | auto (control variates in update

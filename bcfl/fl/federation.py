@@ -286,11 +286,10 @@ class Federation:
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
             self.gossip.tamper = set(cfg.inject_tamper) & set(self.local_clients)
             self.gossip.seed_replicas(self.flat.master)
-        # the clients' AdamW moments persist across rounds when asked for, and under asynchronous
-        # delta exchange: a fresh AdamW per fit (the reference, C8) takes sign-like first steps
-        # every round, and with 8 ranks mixing stale updates the federation then stays on the
-        # plateau (CPU, 8 ranks, lr 5e-4: 0.50 fresh vs 0.995 kept, 2 / 2 runs each; one process:
-        # the same either way)
+        # the clients' AdamW moments persist across rounds when asked for (keep_optimizer_state,
+        # or async_keep_optimizer_state under asynchronous delta exchange: CPU tiny-bert, 8 ranks,
+        # lr 5e-4 learns only with kept moments, 0.50 -> 0.995; MI355X BERT-base at the bench
+        # config the other way round, so it is off by default)
         self.keep_opt = bool(cfg.keep_optimizer_state or (
             cfg.async_keep_optimizer_state and isinstance(self.gossip, MailboxGossip)
             and self.gossip.exchange == "delta"))

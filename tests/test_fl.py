@@ -424,9 +424,9 @@ def test_delta_exchange_matches_state_mixing(tmp_path):
     hosting every client, forced both ways."""
     import torch
     # same optimizer semantics both ways (delta exchange keeps AdamW moments by default)
-    a = _one_rank_run(tmp_path, "state", gossip_exchange="state", keep_optimizer_state=True)
+    a = _one_rank_run(tmp_path, "state", gossip_exchange="state")
     b = _one_rank_run(tmp_path, "delta", gossip_exchange="delta")
-    assert a.gossip.exchange == "state" and b.gossip.exchange == "delta" and a.keep_opt and b.keep_opt
+    assert a.gossip.exchange == "state" and b.gossip.exchange == "delta"
     for c in range(4):
         torch.testing.assert_close(b.client_master[c], a.client_master[c], atol=2e-5, rtol=0)
 
