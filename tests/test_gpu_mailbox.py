@@ -100,3 +100,36 @@ def test_gpu_info_passing_over_mailboxes(tmp_path):
     assert float(r["sync"]) > 0 and float(r["async"]) > 0 and float(r["pred_sync"]) > 0
     assert float(r["bw"][0, 1]) > 1000.0   # MB/s: a device-to-device copy, not a host path
     print({k: v.tolist() for k, v in r.items()})
+
+
+def _server_ckpt_worker(rank, world, out):
+    import json
+    import os
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    cfg = FLConfig(mode="server", model="bert-base-2l", dataset="imdb", num_clients=2,
+                   num_rounds=3, train_samples=64, test_samples=32, global_test_samples=64,
+                   out_dir=out, reference_prints=False, save_every=1, device="cuda",
+                   backend="gloo", overlap_global_eval=True)
+    fed = Federation(cfg, verbose=False)
+    assert fed.eval_stream is not None
+    fed.run()
+    st = None
+    p = os.path.join(out, "global", "state.json")
+    if rank == 0 and os.path.exists(p):
+        st = json.load(open(p))
+    return {"G": fed.global_master.detach().cpu(),
+            "n_acc": torch.tensor(len(st["global_accuracies"]) if st else -1),
+            "acc": torch.tensor(list(fed.global_accuracies))}
+
+
+def test_gpu_server_ranks_checkpoint_with_overlapped_eval(tmp_path):
+    """collective server FedAvg with the overlapped global evaluation AND a
+    checkpoint every round. Only rank 0 writes the checkpoint, but the deferred all-reduce of the
+    evaluation statistics must run on EVERY rank at the same point (else rank 0's 4-element
+    all-reduce pairs with the others' FedAvg all-reduce and hangs or corrupts). Both ranks end on
+    the same global model with the same accuracies, and rank 0's checkpoint carries them."""
+    res = run_world(_server_ckpt_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"))
+    assert torch.equal(res[0]["G"], res[1]["G"])
+    assert torch.equal(res[0]["acc"], res[1]["acc"]) and len(res[0]["acc"]) == 3
+    assert int(res[0]["n_acc"]) >= 2
