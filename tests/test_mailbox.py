@@ -243,3 +243,14 @@ def test_mailbox_async_eight_ranks_bounded_lead_learn_label_shards(tmp_path):
         assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
         assert float(r["wait"]) < 30.0   # the bound holds fast ranks back a little, never stalls
 
+
+
+def test_mailbox_bounded_lead_holds_fast_rank_back(tmp_path):
+    """gossip_max_lead = 1: with one rank slowed by 400 ms per round the fast rank waits at round
+    starts (lead waits > 0) instead of running away, so the staleness it mixes stays within the
+    bound (+1 for the round in flight); unbounded it would drift several rounds ahead."""
+    res = run_world(_learn_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
+                    {"inject_slow": {1: 400.0}, "liveness_timeout": 6, "gossip_max_lead": 1,
+                     "num_rounds": 8})
+    assert float(res[0]["wait"]) > 0.0          # the fast rank was held back
+    assert max(float(r["stale_max"]) for r in res) <= 3.0
