@@ -38,12 +38,7 @@ __device__ __forceinline__ f32x4_t sk_mfma(const bf16x8_t& a, const bf16x8_t& b,
 __device__ __forceinline__ bf16x8_t ld_frag(const bf16_t* p) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
-// the big operand is streamed exactly once: non-temporal loads keep it from evicting the small
-// adapter operand every wave re-reads from L2 (BCFL_SKINNY_NT=1 turns them off for the A/B)
-__device__ __forceinline__ bf16x8_t ld_stream(const bf16_t* p, bool nt) {
-  if (nt) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
-  return *reinterpret_cast<const bf16x8_t*>(p);
-}
+
 
 // ---- skinny_xwt --------------------------------------------------------------------------------
 // part[s, m, c] = sum_{k in slice s} X[m, k] W[c, k],  c < 16 RB (rows of W >= R are clamped:
@@ -52,7 +47,7 @@ template <int RB>
 __global__ __launch_bounds__(256) void skinny_xwt_kernel(const bf16_t* __restrict__ X, int64_t ldx,
                                                          const bf16_t* __restrict__ W, int64_t ldw,
                                                          int M, int K, int R, int kc,
-                                                         float* __restrict__ part, int nt) {
+                                                         float* __restrict__ part) {
   constexpr int RP = 16 * RB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -86,7 +81,7 @@ __global__ __launch_bounds__(256) void skinny_xwt_kernel(const bf16_t* __restric
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) f.x[rb][h] = ld_stream(xr[rb] + k + 32 * h, nt != 0);
+      for (int h = 0; h < 2; ++h) f.x[rb][h] = ld_frag(xr[rb] + k + 32 * h);
 #pragma unroll
     for (int cb = 0; cb < RB; ++cb)
 #pragma unroll
@@ -322,14 +317,13 @@ int skinny_xwt_splits(int M, int K, int* kc) {
 
 int launch_skinny_xwt(const SkinnyParams& p, hipStream_t s) {
   if (p.R < 1 || p.R > 64 || p.K % 64 || p.ldx % 8 || p.ldw % 8 || p.ldo % 8 || !p.part) return -1;
-  static const int nt = skinny_env("BCFL_SKINNY_NT", 2) == 2 ? 1 : 0;  // 1 = off, 2 (default) = on
   const int RB = (p.R + 15) / 16;
   const dim3 grid((p.M + 127) / 128, p.S);
   switch (RB) {
-    case 1: hipLaunchKernelGGL(skinny_xwt_kernel<1>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part, nt); break;
-    case 2: hipLaunchKernelGGL(skinny_xwt_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part, nt); break;
-    case 3: hipLaunchKernelGGL(skinny_xwt_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part, nt); break;
-    default: hipLaunchKernelGGL(skinny_xwt_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part, nt); break;
+    case 1: hipLaunchKernelGGL(skinny_xwt_kernel<1>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part); break;
+    case 2: hipLaunchKernelGGL(skinny_xwt_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part); break;
+    case 3: hipLaunchKernelGGL(skinny_xwt_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part); break;
+    default: hipLaunchKernelGGL(skinny_xwt_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)p.X, p.ldx, (const bf16_t*)p.W, p.ldw, p.M, p.K, p.R, p.kc, p.part); break;
   }
   const int64_t tot = (int64_t)p.M * p.Cz;
   hipLaunchKernelGGL(skinny_reduce_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
