@@ -144,10 +144,24 @@ def _async_mix_desc(fed) -> str:
     return d
 
 
+def _rehearsal_cu_split() -> None:
+    """``BCFL_REHEARSE_CUS=<compute units>``: ranks REHEARSED on one GPU each get a disjoint 1/N of
+    its compute units (ROCr's ``HSA_CU_MASK``, set before the runtime initialises), so N processes
+    behave like N equal, slower GPUs instead of time-slicing the whole chip — the pacing the 8-GPU
+    run has (one rank per GPU), which is what the asynchronous gossip's staleness depends on."""
+    cus = int(os.environ.get("BCFL_REHEARSE_CUS", "0") or 0)
+    w, r = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0"))
+    if cus <= 0 or w <= 1:
+        return
+    per = cus // w
+    os.environ["HSA_CU_MASK"] = f"0:{r * per}-{(r + 1) * per - 1}"
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(a))
+    _rehearsal_cu_split()
     import bcfl  # noqa: F401  (sets the GEMM-library environment before torch initialises it)
     import torch
     from bcfl import ops
@@ -179,6 +193,11 @@ def main():
         fed.run_round(r)
     fed.drain()
     hb[0] = "timed rounds"
+    if fed.is_cuda and rt.world > 1:  # device memory per rank (ranks may share one GPU)
+        free, total = torch.cuda.mem_get_info(fed.device)
+        print(f"[bench] rank {rt.rank}: {torch.cuda.memory_reserved(fed.device) / 2**30:.1f} GiB "
+              f"reserved by torch, device {(total - free) / 2**30:.1f} / {total / 2**30:.1f} GiB used",
+              file=sys.stderr, flush=True)
     D.barrier()
     if fed.is_cuda:
         torch.cuda.synchronize()
