@@ -103,10 +103,17 @@ class FLConfig:
                                         # delta for multi-rank async gossip on complete graphs
     gossip_apply_on_arrival: bool = True  # delta exchange: apply neighbours' updates between
                                           # local steps as they arrive (non-blocking polls)
-    gossip_max_lead: int = 2            # async mailbox gossip: bounded staleness (SSP) — do not
+    gossip_max_lead: int = 1            # async mailbox gossip: bounded staleness (SSP) — do not
     #                                     start a round while a live neighbour's newest applied
-    #                                     update is > this many rounds behind (0 = unbounded)
+    #                                     update is > this many rounds behind (0 = unbounded).
+    #                                     8 ranks on equal CU slices of one MI355X: 1 learns
+    #                                     (0.73 / 0.95 / 0.77), 2 does not (0.50 / 0.50);
+    #                                     profiles/multirank_cu_split_r4.json
     gossip_lead_timeout_s: float = 5.0  # ... a neighbour still behind after this counts as dead
+    gossip_self_delay: str = "off"      # delta exchange, async: "on" applies this rank's OWN
+    #                                     updates one round late, at the mix where the neighbours'
+    #                                     same-round updates land, so every model holds complete
+    #                                     rounds (no own-shard tilt on label shards) | "off"
     gossip_stale_decay: float = 0.0     # async mailbox mix: a view k rounds behind keeps
                                         # W / (1 + decay * k) of its weight (rest -> self)
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
@@ -192,6 +199,7 @@ class FLConfig:
                    "drift_exchange": ("auto", "on", "off"),
                    "gossip_exchange": ("auto", "state", "delta"),
                    "drift_stale_compensation": ("none", "own", "global"),
+                   "gossip_self_delay": ("off", "on"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
                    "fedavg_weighting": ("examples", "batches", "uniform"),

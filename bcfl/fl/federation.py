@@ -256,6 +256,8 @@ class Federation:
                                                 exchange=exch)
                     self.drift.stale_compensation = cfg.drift_stale_compensation
                     self.gossip.stale_decay = float(cfg.gossip_stale_decay)
+                    if cfg.gossip_self_delay == "on" and self.gossip.exchange == "delta":
+                        self.gossip.enable_self_delay()
                 except MailboxUnavailable as e:
                     # every rank sees the same outcome (agreed collectively in the transport):
                     # fall back together to the lock-step RCCL engine

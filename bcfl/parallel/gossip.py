@@ -455,6 +455,20 @@ class MailboxGossip:
         self._apply_events: List = []
         self._started: set = set()
         self.applied_mid = 0
+        self.pend: Optional[Dict[int, torch.Tensor]] = None   # see enable_self_delay
+
+    def enable_self_delay(self) -> None:
+        """Delta exchange: this rank's OWN updates (every hosted client's u_c of round r) enter
+        the hosted models one round late, at the round-(r + 1) mix — about when the remote
+        neighbours' round-r updates, fetched and applied during round r + 1, have landed. Every
+        model then holds (nearly) complete rounds of updates. Without it a model holds its own
+        latest update a round before the others' of the same round: on label shards that is a
+        tilt toward its own class that the same round's opposite-class updates have not yet
+        cancelled, and on a weak early signal it decides the model's predictions."""
+        if self.exchange != "delta":
+            raise ValueError("self delay applies to the delta exchange")
+        self.pend = {c: torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+                     for c in self.local}
 
     # ------------------------------------------------------------------------------------
     def seed_replicas(self, initial: torch.Tensor):
@@ -717,14 +731,17 @@ class MailboxGossip:
         for j, snap in self._fresh.items():
             tau = max(0, round_idx - snap.round)
             damp[j] = 1.0 / (1.0 + self.stale_decay * max(0, tau - 1))
+        own = self.pend if self.pend is not None else self.start
         for c in self.local:
-            views = [self.start[c]]
-            ws = [-(1.0 - float(W[c, c]))]
+            if self.pend is not None:   # y_c - u_c + W_cc u_c(previous round)
+                views, ws = [self.start[c], self.pend[c]], [-1.0, float(W[c, c])]
+            else:
+                views, ws = [self.start[c]], [-(1.0 - float(W[c, c]))]
             for j in range(self.n):
                 if j == c or W[c, j] == 0.0:
                     continue
                 if j in self.states:
-                    views.append(self.start[j])
+                    views.append(own[j])
                     ws.append(float(W[c, j]))
                 elif j in self._fresh:
                     wj = float(W[c, j]) * damp[j]
@@ -737,6 +754,9 @@ class MailboxGossip:
         for j in list(self._fresh):   # the new snapshot becomes the applied one
             self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
         self._fresh = {}
+        if self.pend is not None:     # this round's own updates wait for the next mix
+            for c in self.local:      # (start[c] is re-recorded at the next round's start)
+                self.pend[c], self.start[c] = self.start[c], self.pend[c]
 
     def _age_weighted(self, W: np.ndarray, round_idx: int) -> np.ndarray:
         """``stale_decay`` > 0: a neighbour view k rounds behind keeps W_cj / (1 + decay * k) of
@@ -824,6 +844,8 @@ class MailboxGossip:
         self._inflight = None          # an unapplied mid-round fetch is simply fetched again
         t = lambda d: {int(k): v.detach().cpu().clone() for k, v in d.items()}  # noqa: E731
         st = {"cum": t(self.cum)} if self.exchange == "delta" else {}
+        if self.pend is not None:
+            st["pend"] = t(self.pend)
         return {**st,
                 "send_buf": {int(c): [b.detach().cpu().clone() for b in v] for c, v in self.send_buf.items()},
                 "replica": t(self.replica), "version": dict(self.version), "steps": dict(self.steps),
@@ -840,6 +862,9 @@ class MailboxGossip:
         if self.exchange == "delta" and "cum" in st:
             for c, v in st["cum"].items():
                 self.cum[int(c)].copy_(v.to(self.device))
+        if self.pend is not None and "pend" in st:
+            for c, v in st["pend"].items():
+                self.pend[int(c)].copy_(v.to(self.device))
         for name in ("version", "steps", "applied", "replica_round"):
             getattr(self, name).update({int(k): int(v) for k, v in st[name].items()})
         self.dead = set(int(x) for x in st["dead"])

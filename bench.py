@@ -170,6 +170,10 @@ def main():
     from bcfl.parallel import dist as D
 
     rt = D.init_runtime(a.device)
+    if os.environ.get("BCFL_REHEARSE_CUS") and rt.world > 1 and torch.cuda.is_available():
+        # N ranks share one GPU's HBM: cap each caching allocator (it keeps ~2x its peak cached
+        # across its streams) so N of them plus the mailboxes fit
+        torch.cuda.set_per_process_memory_fraction(0.7 / rt.world)
     if rt.world != a.gpus:
         raise SystemExit(f"bench.py --gpus {a.gpus} but the job has WORLD_SIZE={rt.world}: "
                          "launch one rank per GPU (torch.distributed.run --nproc-per-node N)")

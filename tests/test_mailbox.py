@@ -131,9 +131,11 @@ def test_mailbox_tamper_rejected_and_logged(tmp_path):
 
 
 def test_mailbox_slow_peer_does_not_stall(tmp_path):
-    # client 1 (rank 1) sleeps 5 s per round; rank 0 keeps its own pace
+    # client 1 (rank 1) sleeps 5 s per round; rank 0 keeps its own pace (unbounded staleness:
+    # with the default bound a 5 s/round peer holds the fast rank back by design, see
+    # test_mailbox_bounded_lead_holds_fast_rank_back)
     res = run_world(_fed_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"inject_slow": {1: 5000.0}, "num_rounds": 3})
+                    {"inject_slow": {1: 5000.0}, "num_rounds": 3, "gossip_max_lead": 0})
     assert float(res[1]["times"].min()) >= 5.0
     # the first round includes setup (mailbox mapping, first exchange) and is slow on a loaded
     # CPU; every later round of rank 0 runs at its own pace, and its whole run ends well before
@@ -232,10 +234,10 @@ def test_mailbox_async_eight_ranks_bounded_lead_learn_label_shards(tmp_path):
     up 4-6 rounds apart and the fast ones train mostly on their own label shard; at this learning
     rate a fresh AdamW per round (the reference's per-fit optimizer) then stays on the plateau
     (0.50 in 2 / 2 runs), so the test keeps the moments (async_keep_optimizer_state; off by
-    default: the MI355X bench config prefers fresh AdamW). Bounded staleness (gossip_max_lead = 2,
-    default) + kept moments learn (0.995, 3 / 3)."""
+    default: the MI355X bench config prefers fresh AdamW). Bounded staleness (gossip_max_lead = 2)
+    + kept moments learn (0.995, 3 / 3)."""
     res = run_world(_learn_worker, 8, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"num_clients": 8, "num_rounds": 24, "lr": 5e-4,
+                    {"num_clients": 8, "num_rounds": 24, "lr": 5e-4, "gossip_max_lead": 2,
                      "async_keep_optimizer_state": True})
     for r in res:
         assert not r["same_round"] and r["exchange"] and r["delta"]
@@ -243,6 +245,31 @@ def test_mailbox_async_eight_ranks_bounded_lead_learn_label_shards(tmp_path):
         assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
         assert float(r["wait"]) < 30.0   # the bound holds fast ranks back a little, never stalls
 
+
+
+def test_mailbox_self_delay_runs_and_resumes_state(tmp_path):
+    """gossip_self_delay = on (opt-in): a rank's own updates enter its models one round late;
+    the federation still runs its async rounds and the pending updates are part of the gossip
+    resume state."""
+    res = run_world(_self_delay_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), {})
+    for r in res:
+        assert bool(r["pend_in_state"])
+        assert torch.isfinite(r["acc"]).all()
+
+
+def _self_delay_worker(rank, world, out, kw):
+    from bcfl.config import get_preset
+    from bcfl.fl import Federation
+    torch.set_num_threads(2)
+    fed = Federation(get_preset("baseline3_learnable", model="tiny-bert", num_clients=4, num_rounds=4,
+                                mode="serverless", max_seq_len=64, train_samples=64,
+                                global_test_samples=64, eval_local=False, save_every=0,
+                                ledger=False, device="cpu", reference_prints=False, out_dir=out,
+                                backend="gloo", gossip_transport="mailbox",
+                                gossip_self_delay="on"), verbose=False)
+    fed.run()
+    return {"pend_in_state": torch.tensor("pend" in fed.gossip.state_dict()),
+            "acc": torch.tensor([x["global_acc"] for x in fed.history])}
 
 
 def test_mailbox_bounded_lead_holds_fast_rank_back(tmp_path):
