@@ -197,6 +197,10 @@ class AsyncCheckpointer:
         def _write():
             if done is not None:
                 done.synchronize()
+                # one snapshot stays for the next save; the extra ones of a multi-model save
+                # (save_clients: one per hosted client) go back to the allocator now that their
+                # D2H copies are done — not kept model-sized in HBM for the whole run
+                del self.snaps[1:]
             st = state
             if st is not None and callable(st.get("_finalize")):
                 # fields only known once device work queued before the save has finished (e.g. an

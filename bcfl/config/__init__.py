@@ -44,10 +44,11 @@ class FLConfig:
                                         # disjoint 1/num_clients stride of the global draw (MEAN
                                         # CLIENT ACCURACY of the federation; total eval work
                                         # independent of the GPU count); "average" = the mean of
-                                        # the rank's hosted client models on the whole draw (the
-                                        # reference's global_model, serverless_NonIID_IMDB.py:
-                                        # 296-304); "client0" = each rank's first client model on
-                                        # the whole draw
+                                        # ALL client models on the whole draw (the reference's
+                                        # global_model, serverless_NonIID_IMDB.py:296-304; one
+                                        # process only: with several ranks no rank holds every
+                                        # client model); "client0" = each rank's first client
+                                        # model on the whole draw
     dirichlet_alpha: float = 0.5
     resample_each_round: bool = False   # reference IID scripts draw a fresh random sample every round
     synthetic_signal: Optional[float] = None  # planted class tokens per 64 (None = generator default)
@@ -117,7 +118,20 @@ class FLConfig:
     gossip_stale_decay: float = 0.0     # async mailbox mix: a view k rounds behind keeps
                                         # W / (1 + decay * k) of its weight (rest -> self)
     gossip_transport: str = "auto"      # auto | mailbox (one-sided hipIpc/shm inboxes) | rccl
-                                        # (matched send/recv); auto = mailbox when async, else rccl
+                                        # (matched send/recv) | loopback (ONE process: every hosted
+                                        # client its own virtual rank, posts visible after
+                                        # loopback_lag_steps — the multi-rank async protocol on one
+                                        # GPU); auto = mailbox when async, else rccl
+    loopback_lag_steps: List[int] = field(default_factory=lambda: [1, 2])  # [lo, hi]: a post
+    #                                     becomes visible U{lo..hi} local-step ticks after it was
+    #                                     made (0 = at once: the round-end collect sees every post)
+    gossip_apply_scale: float = 1.0     # delta exchange: fraction of the neighbours' (and own) mean
+    #                                     update a model takes in (outer step size; 1 = the mean)
+    gossip_apply: str = "arrival"       # delta exchange: "arrival" = each neighbour's new progress
+    #                                     is applied as soon as it lands | "complete" = the round-T
+    #                                     posts of ALL live sources (own included) are applied
+    #                                     together once the last has landed, so every model holds
+    #                                     complete rounds (no partial-round class tilt)
     verify_updates: bool = True         # receivers re-hash every received payload vs its root
     wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
@@ -157,7 +171,9 @@ class FLConfig:
     # --- io / observability -----------------------------------------------------------
     out_dir: str = "runs/default"
     save_every: int = 1
-    save_clients: bool = False          # also <out>/client_{k}/ for every hosted client
+    save_clients: bool = False          # also <out>/client_{k}/ for every hosted client (each
+    #                                     save holds one fp32 device snapshot per hosted client
+    #                                     until its host copy is done, then frees all but one)
     save_resume_state: bool = False     # also <out>/resume/rank{r}.pt (clients, optimizer, RNG, gossip)
     compat_save_path: Optional[str] = None   # e.g. "my_albert_model2"
     async_ckpt: bool = True
@@ -192,7 +208,8 @@ class FLConfig:
     def __post_init__(self):
         choices = {"mode": ("server", "serverless"), "mixing": ("average", "metropolis"),
                    "topology": ("full", "ring", "pagerank"),
-                   "gossip_transport": ("auto", "mailbox", "rccl"),
+                   "gossip_transport": ("auto", "mailbox", "rccl", "loopback"),
+                   "gossip_apply": ("arrival", "complete"),
                    "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
                    "server_transport": ("rccl", "mailbox"),
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),

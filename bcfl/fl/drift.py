@@ -195,6 +195,20 @@ class DriftCorrection:
             ops.axpby_(d, self.cv[c], -1.0, 1.0)
         self.ready[c] = True
 
+    @torch.no_grad()
+    def set_correction(self, c: int, views: Sequence[torch.Tensor], weights: Sequence[float]) -> None:
+        """Exchange mode, round-complete gossip (:meth:`bcfl.parallel.gossip.MailboxGossip.
+        _refresh_aux`): ``d_c = sum_j w_j c_j`` with every term from the same applied round
+        (the client's own control variate enters with weight ``W_cc - 1``)."""
+        if not (self.enabled and self.exchange):
+            return
+        d = self.buf[c]
+        d.zero_()
+        if views:
+            ops.gossip_mix_(d, list(views), 0.0, [float(w) for w in weights])
+        self.ready[c] = True
+        self.lr_sum.pop(c, None)
+
     def after_exchange(self, c: int, self_w: float, views: Sequence[torch.Tensor],
                        weights: Sequence[float]) -> None:
         """:meth:`begin` + :meth:`end` without a model mix in between."""

@@ -190,8 +190,18 @@ class Federation:
             self.global_master = self.flat.master.detach().clone()
             self.acc = torch.zeros_like(self.flat.master)
         # ---------------- gossip -------------------------------------------------------------------
-        if cfg.gossip_transport not in ("auto", "mailbox", "rccl"):
+        if cfg.gossip_transport not in ("auto", "mailbox", "rccl", "loopback"):
             raise ValueError(f"unknown gossip_transport {cfg.gossip_transport!r}")
+        if cfg.global_eval_models == "average" and cfg.mode == "serverless" and self.rt.distributed:
+            # the reference's averaged global_model needs every client model; a rank only holds
+            # its own (averaging its partial set and all-reducing the scores would report the
+            # mean accuracy of partial averages, not the federation average's — ADVICE r4)
+            raise ValueError("global_eval_models='average' scores the mean of ALL client models "
+                             "and needs world 1; with several ranks use 'all' (every client model "
+                             "on its stride of the draw) or 'client0'")
+        if cfg.gossip_transport == "loopback" and (self.rt.distributed or not cfg.async_gossip):
+            raise ValueError("gossip_transport='loopback' runs the asynchronous multi-rank protocol "
+                             "inside ONE process (world 1, async_gossip=True)")
         # drift correction across ranks: async mailbox gossip exchanges the clients' control
         # variates with their models (stale-exact SCAFFOLD, fl/drift.py) and never waits;
         # FLConfig.drift_same_round_mix instead waits for every neighbour's round-r snapshot
@@ -202,15 +212,19 @@ class Federation:
         if self.transport == "auto":
             # deterministic: the lock-step engine mixes exactly the previous round's states
             self.transport = "mailbox" if (cfg.async_gossip and not cfg.deterministic) else "rccl"
+        loopback = self.transport == "loopback"
+        # several ranks, or one process whose hosted clients are virtual ranks: the mixes are
+        # stale, so the asynchronous protocol's exchanges apply
+        multi_rank = self.rt.distributed or loopback
         cv_exchange = (cfg.mode == "serverless" and not cfg.compat_chain and self.drift.enabled
-                       and self.transport == "mailbox"
+                       and self.transport in ("mailbox", "loopback")
                        and (cfg.drift_exchange == "on" or (
-                           cfg.drift_exchange == "auto" and self.rt.distributed
+                           cfg.drift_exchange == "auto" and multi_rank
                            and cfg.async_gossip and not self.same_round_mix)))
         # A mailbox federation never waits on a peer: the per-round path is collective-free
         # (metrics, evaluation and ledger are rank-local) so a slow or exited rank cannot stall
         # the others. The update anomaly filter needs a global view and keeps its collectives.
-        self.collective_free = (cfg.mode == "serverless" and self.transport == "mailbox"
+        self.collective_free = (cfg.mode == "serverless" and self.transport in ("mailbox", "loopback")
                                 and cfg.anomaly_filter == "none" and not cfg.compat_chain)
         # server FedAvg over mailboxes (liveness: a dead rank is left out, weights re-normalised)
         self.server_mbox = None
@@ -221,6 +235,8 @@ class Federation:
                 self.server_mbox = MailboxFedAvg(self.flat.numel, self.device,
                                                  cfg.server_timeout_s, cfg.verify_updates)
         self.excluded: List[int] = []
+        self.skipped_epochs = 0            # mailbox FedAvg: aggregation epochs this rank missed
+        self.final_check: Optional[dict] = None
         self._lead_gone: Dict[int, int] = {}   # bounded staleness: neighbours given up on
         self.gossip: Optional[GossipEngine] = None
         if cfg.mode == "serverless" and not cfg.compat_chain:
@@ -230,13 +246,13 @@ class Federation:
             self.nbrs = neighbours(cfg.topology, n, self.excluded)
             states = ({c: self.client_master[c] for c in self.local_clients} if self.multi
                       else {self.local_clients[0]: self.flat.master})
-            if self.transport == "mailbox":
+            if self.transport in ("mailbox", "loopback"):
                 aux = self.drift.use_exchange() if cv_exchange else None
                 exch = cfg.gossip_exchange
                 if exch == "auto":
                     # delta exchange where snapshots can be stale: several ranks, async, and a
                     # complete neighbour graph (applying every update once needs everyone's)
-                    exch = ("delta" if (self.rt.distributed and cfg.async_gossip
+                    exch = ("delta" if (multi_rank and cfg.async_gossip
                                         and not self.same_round_mix
                                         and cfg.topology in ("full", "pagerank")) else "state")
                 if exch == "delta" and cfg.topology == "ring":
@@ -251,11 +267,17 @@ class Federation:
                                                 # (its later posts bring it back), not waited on
                                                 sync_timeout_s=10.0 if self.same_round_mix else 60.0,
                                                 liveness_timeout=cfg.liveness_timeout,
-                                                verify=cfg.verify_updates, aux=aux,
+                                                # in-process posts cross no link: nothing to verify
+                                                verify=cfg.verify_updates and not loopback, aux=aux,
                                                 aux_sink=self.drift if aux else None,
-                                                exchange=exch)
+                                                exchange=exch,
+                                                apply=cfg.gossip_apply if exch == "delta" else "arrival",
+                                                virtual=loopback,
+                                                lag_steps=tuple(cfg.loopback_lag_steps),
+                                                seed=cfg.seed)
                     self.drift.stale_compensation = cfg.drift_stale_compensation
                     self.gossip.stale_decay = float(cfg.gossip_stale_decay)
+                    self.gossip.apply_scale = float(cfg.gossip_apply_scale)
                     if cfg.gossip_self_delay == "on" and self.gossip.exchange == "delta":
                         self.gossip.enable_self_delay()
                 except MailboxUnavailable as e:
@@ -266,7 +288,7 @@ class Federation:
                     self.transport = "rccl"
                     self.collective_free = False
                     self.drift.drop_exchange()
-            if self.transport != "mailbox":
+            if self.transport not in ("mailbox", "loopback"):
                 wire = cfg.wire_dtype if cfg.wire_dtype != "bf16" else "bf16_delta"
                 if cfg.wire_dtype == "bf16_raw":
                     wire = "bf16"
@@ -281,9 +303,14 @@ class Federation:
                 if self.gossip.exchange == "delta" and self.drift.exchange:
                     # the gossip's round-start records double as the drift correction's x_c
                     self.drift.start_of = self.gossip.start
-                # apply on arrival: neighbours' updates enter between local steps (delta exchange)
+                # apply on arrival: neighbours' updates enter between local steps (delta exchange).
+                # Not with the update anomaly filter or Byzantine injection: a mid-round
+                # application would fold a neighbour's update into the model before this round's
+                # verdict on it exists (the round-end mix applies verdicted weights only)
                 self.gossip.W_mid = mixing_matrix(self.nbrs, cfg.mixing)
-                self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival)
+                self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival
+                                                     and cfg.anomaly_filter == "none"
+                                                     and not cfg.inject_byzantine)
                 self.gossip._also = self._mid_round_targets
             self.gossip.suppressed = set(cfg.inject_drop) & set(self.local_clients)
             self.gossip.tamper = set(cfg.inject_tamper) & set(self.local_clients)
@@ -455,7 +482,7 @@ class Federation:
         gone = self._lead_gone
 
         def seen(j):
-            return max(g.replica_round[j], posted.get(j, -1))
+            return max(g.replica_round[j], posted.get(j, -1), g.seen_round.get(j, -1))
 
         def lag():
             for j in [j for j in gone if seen(j) > gone[j]]:
@@ -533,9 +560,10 @@ class Federation:
                 self._phase[c] = "trained"
                 self.drift.detach(lane.opt)
                 if prev is not None:
-                    self._inject_byzantine(c, prev, lane.flat)
+                    ref = self._update_ref(c, prev)
+                    self._inject_byzantine(c, ref, lane.flat)
                     if self.filter is not None:
-                        out["sk"][c], out["nr"][c] = self._update_stats(prev, lane.flat)
+                        out["sk"][c], out["nr"][c] = self._update_stats(ref, lane.flat)
                 out["losses"][c] = st
                 if cfg.eval_local:
                     out["local_eval"][c] = lane.trainer.evaluate_device(self.test_batches(c, r))
@@ -915,6 +943,16 @@ class Federation:
             time.sleep(self.cfg.inject_slow[c] / 1000.0)
         return out
 
+    def _update_ref(self, c: int, prev: torch.Tensor) -> torch.Tensor:
+        """What client c's own update of the round is measured from: the round-start copy, or —
+        delta-exchange gossip — the gossip's round-start record, which also carries every
+        neighbour update applied to the model during the round (so sketches, norms and injected
+        scaling see this client's own progress only)."""
+        g = self.gossip
+        if isinstance(g, MailboxGossip) and g.exchange == "delta" and c in g._started:
+            return g.start[c]
+        return prev
+
     @torch.no_grad()
     def _inject_byzantine(self, c: int, ref: torch.Tensor, flat: Optional[FlatParams] = None):
         s = self.cfg.inject_byzantine.get(c)
@@ -1200,9 +1238,18 @@ class Federation:
         extra = {"kind": "global", "root": self._merkle() if self.ledger else "",
                  "rejected": sorted(v.rejected)}
         if self.server_mbox is not None:
+            sk = int(self._server_live.get("epochs_skipped", 0))
             extra.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
                          rejoined_ranks=self._server_live["rejoined_ranks"],
-                         view_mismatch=self._server_live["view_mismatch"])
+                         view_mismatch=self._server_live["view_mismatch"],
+                         epoch=int(self._server_live.get("epoch", r + 1)), epochs_skipped=sk)
+            if sk:
+                # this rank joined a later aggregation epoch (started late / excluded as slow):
+                # the skipped epochs were aggregated WITHOUT it and are not trained rounds here
+                self.skipped_epochs += sk
+                warnings.warn(f"round {r}: this rank joined aggregation epoch "
+                              f"{self._server_live.get('epoch')} and skipped {sk} epoch(s) the "
+                              "federation aggregated without it", RuntimeWarning)
             if self._server_live["view_mismatch"]:
                 warnings.warn(f"round {r}: rank(s) {self._server_live['view_mismatch']} aggregated "
                               "a different live-rank set last round than this rank (a timed-out "
@@ -1215,6 +1262,7 @@ class Federation:
         if self.server_mbox is not None:
             out.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
                        dead_peers=sorted(self.server_mbox.dead),
+                       epochs_skipped=int(self._server_live.get("epochs_skipped", 0)),
                        view_mismatch=self._server_live["view_mismatch"],
                        rejoined_ranks=self._server_live["rejoined_ranks"])
         return out
@@ -1293,10 +1341,11 @@ class Federation:
             self._phase[c] = "trained"
             self.drift.detach(self.opt)
             if prev is not None:
-                self._inject_byzantine(c, prev)
+                ref = self._update_ref(c, prev)
+                self._inject_byzantine(c, ref)
                 if self.filter is not None:
                     with self.timer.phase("anomaly"):
-                        sk[c], nr[c] = self._update_stats(prev)
+                        sk[c], nr[c] = self._update_stats(ref)
             losses[c] = st
             if cfg.eval_local:
                 with self.timer.phase("eval_local"):
@@ -1528,7 +1577,8 @@ class Federation:
                "dead_peers": res.get("dead_peers", []),
                **{k: res[k] for k in ("mixed", "stale_rounds", "stale_max", "wait_s", "lead_wait_s", "torn",
                                       "rejected_msgs", "absent_ranks", "live_weight",
-                                      "view_mismatch", "rejoined_ranks") if k in res},
+                                      "view_mismatch", "rejoined_ranks", "epochs_skipped",
+                                      "applied_round", "post_lag_rounds") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}
         if self.is_cuda:
@@ -1690,6 +1740,31 @@ class Federation:
                     mismatched += int(committed[key] != b["update_root"])
         return {"checked": checked, "mismatched": mismatched, "rejected": rejected}
 
+    def _final_model_check(self) -> dict:
+        """Mailbox FedAvg: every rank's FINAL global model root, gathered (a collective, run once
+        at the end). Ranks that aggregated different live sets in the last round(s) — a slow rank
+        timed out by a fast one that then finished — end on different models; that split is
+        recorded in every rank's ledger and warned about, never silent."""
+        root = ops.merkle_root_sha256(self.global_master).hex()
+        allr = D.all_gather_object({"rank": self.rt.rank, "root": root,
+                                    "rounds": len(self.history), "epoch": self.server_mbox.epoch,
+                                    "skipped_epochs": self.skipped_epochs})
+        roots = [x["root"] for x in allr]
+        split = len(set(roots)) > 1
+        info = {"split": split, "ranks": allr}
+        if self.ledger is not None:
+            self.ledger.append(len(self.history), -1, "final_check", root,
+                               "reject" if split else "accept", info, ts=float(len(self.history) + 1))
+            self.ledger.flush()
+        if split:
+            groups = {}
+            for x in allr:
+                groups.setdefault(x["root"][:16], []).append(x["rank"])
+            warnings.warn(f"mailbox FedAvg ended SPLIT: the ranks hold {len(groups)} different "
+                          f"final global models {sorted(groups.values())} (a live-set "
+                          "disagreement in the last aggregation epoch)", RuntimeWarning)
+        return info
+
     def finish(self, audit: bool = True):
         """Drain communication and I/O, verify the ledger (collective-free runs: cross-rank audit,
         a collective — pass ``audit=False`` when some rank has exited)."""
@@ -1707,6 +1782,8 @@ class Federation:
                 if self.ledger_audit["mismatched"]:
                     raise RuntimeError(f"ledger audit: {self.ledger_audit['mismatched']} accepted "
                                        "updates do not match their sender's commitment")
+        if self.server_mbox is not None and self.rt.distributed and audit:
+            self.final_check = self._final_model_check()
         tel = self.telemetry.finish()
         if self.verbose and self.cfg.reference_prints:
             gdir = os.path.join(self.cfg.out_dir, "global")

@@ -385,7 +385,8 @@ class MailboxGossip:
                  wire: str = "bf16", sync: bool = False, liveness_timeout: int = 2,
                  verify: bool = True, sync_timeout_s: float = 60.0, rank: Optional[int] = None,
                  world: Optional[int] = None, aux: Optional[Dict[int, torch.Tensor]] = None,
-                 aux_sink=None, exchange: str = "state"):
+                 aux_sink=None, exchange: str = "state", apply: str = "arrival",
+                 virtual: bool = False, lag_steps=(1, 1), seed: int = 0):
         from .mailbox import MailboxTransport
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
@@ -410,24 +411,57 @@ class MailboxGossip:
             raise ValueError("aux states must cover exactly the hosted clients")
         self.msg_numel = self.numel * (2 if aux is not None else 1)
         self.wire_dtype = torch.float32 if wire == "fp32" else torch.bfloat16
-        self.remote_needed = sorted({j for c in self.local for j in nbrs[c]
-                                     if client_rank(j, self.world) != self.rank})
+        if apply not in ("arrival", "complete"):
+            raise ValueError(f"apply must be 'arrival' or 'complete', got {apply!r}")
+        if apply == "complete" and exchange != "delta":
+            raise ValueError("round-complete application applies cumulative updates (exchange='delta')")
+        self.apply_mode = apply
+        # virtual ranks (in-process loopback transport): every hosted client is its own rank, so
+        # every OTHER client is remote to it — updates arrive late, through the transport
+        self.virtual = bool(virtual)
+        complete = apply == "complete"
+        if self.virtual:
+            self.remote_needed = sorted({j for c in self.local for j in nbrs[c]}
+                                        | (set(self.local) if complete else set()))
+        else:
+            self.remote_needed = sorted({j for c in self.local for j in nbrs[c]
+                                         if client_rank(j, self.world) != self.rank})
         send_plan = []
         for c in self.local:
             dsts = sorted({client_rank(i, self.world) for i in range(self.n) if c in nbrs[i]}
                           - {self.rank})
             send_plan += [(c, r) for r in dsts]
-        self.transport = MailboxTransport(self.msg_numel, self.wire_dtype, self.device,
-                                          self.remote_needed, send_plan, self.rank, self.world)
+        if self.virtual:
+            from .loopback import LoopbackTransport
+            self.transport = LoopbackTransport(self.msg_numel, self.wire_dtype, self.device,
+                                               self.local, lag_steps, seed)
+        else:
+            self.transport = MailboxTransport(self.msg_numel, self.wire_dtype, self.device,
+                                              self.remote_needed, send_plan, self.rank, self.world)
         z = lambda: torch.zeros(self.msg_numel, dtype=self.wire_dtype, device=self.device)  # noqa: E731
         self.send_buf = {c: [z(), z()] for c in self.local}
         self.replica = {j: z() for j in self.remote_needed}
         self.stage = {j: z() for j in self.remote_needed}
+        # round-complete application: every source's applied snapshot is held in a replica, the
+        # hosted clients' own posts included (their send slots are read where they are)
+        self.sources = sorted(set(self.remote_needed) | (set(self.local) if complete else set()))
+        if complete:
+            for c in self.local:
+                if c not in self.replica:
+                    self.replica[c] = z()
+        self.apply_scale = 1.0   # delta exchange: fraction of the federation's mean update applied
+        self.applied_T = -1                                  # newest round applied everywhere
+        self.seen_round = {j: -1 for j in self.sources}      # newest round each source posted
+        self.slot_meta = {c: [(0, -1), (0, -1)] for c in self.local}   # (version, round) per slot
+        self._last_round = -1
         self.liveness_timeout = liveness_timeout
         self.version = {c: 0 for c in self.local}
         self.steps = {c: 0 for c in self.local}
-        self.applied = {j: 0 for j in self.remote_needed}     # version held in replica[j]
-        self.replica_round = {j: -1 for j in self.remote_needed}
+        self.applied = {j: 0 for j in self.sources}           # version held in replica[j]
+        # newest version of each source that failed verification: never fetched (or ledgered)
+        # again — a tampering neighbour costs one re-hash per version, not one per local step
+        self.rejected_version = {j: 0 for j in self.sources}
+        self.replica_round = {j: -1 for j in self.sources}
         self.suppressed: set = set()
         self.tamper: set = set()     # fault injection: corrupt these clients' payloads after hashing
         self.dead: set = set()
@@ -477,8 +511,7 @@ class MailboxGossip:
         the staleness bound retires it (delta exchange: version 0 = no progress, S = 0). Aux
         halves (control variates) start at zero."""
         n = self.numel
-        for t in [self.replica[j] for j in self.remote_needed] + \
-                 [b for c in self.local for b in self.send_buf[c]]:
+        for t in list(self.replica.values()) + [b for c in self.local for b in self.send_buf[c]]:
             if self.exchange == "delta":
                 t[:n].zero_()
             else:
@@ -497,6 +530,14 @@ class MailboxGossip:
             self._started.add(c)
 
     # ---- apply on arrival ---------------------------------------------------------------------
+    def _want(self, js) -> Dict[int, int]:
+        """Fetch only versions newer than both the applied and the last rejected one."""
+        return {j: max(self.applied[j], self.rejected_version[j]) for j in js}
+
+    def _reject(self, j: int, version: int) -> None:
+        self.rejected_msgs += 1
+        self.rejected_version[j] = max(self.rejected_version[j], int(version))
+
     def _hash(self, t: torch.Tensor):
         return ops.merkle_root_deferred(t)
 
@@ -513,14 +554,17 @@ class MailboxGossip:
         buffers ``also(c)`` returns; then the next fetch starts. Called between local steps, so
         a neighbour's update enters a round or more earlier than at the round's end mix.
         Returns the number of snapshots applied."""
-        if not (self.apply_on_arrival and self.remote_needed) or self.W_mid is None:
-            return 0
         tr = self.transport
+        if self.virtual:
+            tr.tick()                 # one local step of every lane: the in-process clock
+        if not (self.apply_on_arrival and self.sources) or self.W_mid is None:
+            return 0
+        if self.apply_mode == "complete":
+            return self._poll_complete(streams, param_out)
         h = self._inflight
         if h is None:
             md = getattr(self, "_mix_done", None)   # the round-end mix read stage / replica too
-            self._inflight = tr.fetch_begin({j: self.applied[j] for j in self.remote_needed},
-                                            self.stage,
+            self._inflight = tr.fetch_begin(self._want(self.remote_needed), self.stage,
                                             after=self._apply_events + ([md] if md is not None else []))
             self._apply_events = []
             h = self._inflight
@@ -555,7 +599,7 @@ class MailboxGossip:
             self.records.append({"client": j, "kind": "recv", "version": snap.version,
                                  "root": snap.root.hex(), "ok": ok, "src_round": snap.round})
             if not ok:
-                self.rejected_msgs += 1
+                self._reject(j, snap.version)
                 continue
             good[j] = snap
         if not good:
@@ -565,9 +609,10 @@ class MailboxGossip:
         for c in self.local:
             views, ws, aviews = [], [], []
             for j in good:
-                if W[c, j] != 0.0:
+                if W[c, j] != 0.0 and self._remote(c, j):
                     views += [self.stage[j][:n], self.replica[j][:n]]
-                    ws += [float(W[c, j]), -float(W[c, j])]
+                    wj = float(W[c, j]) * self.apply_scale
+                    ws += [wj, -wj]
                     if self.aux is not None:
                         aviews += [self.stage[j][n:], self.replica[j][n:]]
             if not views:
@@ -598,8 +643,217 @@ class MailboxGossip:
         self.applied_mid += len(good)
         return len(good)
 
-    def _msg(self, j: int) -> torch.Tensor:
-        if j in self.states:
+    # ---- round-complete application (apply="complete") ---------------------------------------
+    # Every model holds COMPLETE rounds of the federation's updates: the round-T posts of every
+    # live source (this rank's own clients included) are applied together, once the last of them
+    # has landed, and a client's own update leaves its live model at the round end until its
+    # round is complete. With label shards each post pulls towards one class; a model that holds
+    # some sources' round-r updates and not others' is tilted towards whichever classes arrived
+    # first (8 ranks on CU slices: 0.73-0.95 final accuracy, multirank_cu_split_r4.json). Here
+    # nothing ever waits: training continues on the last complete base while a round is in
+    # flight, and with every post visible at the round end the result is exactly the synchronous
+    # mean (FedAvg with the reference's unweighted average, serverless_NonIID_IMDB.py:296).
+
+    def _gate(self, remote_rounds: Dict[int, int]) -> Optional[int]:
+        """Newest round every live source has posted (``None``: not newer than the one applied).
+        A source silent for more than ``liveness_timeout`` rounds stops holding rounds back."""
+        seen = self.seen_round
+        for j, rr in remote_rounds.items():
+            if rr > seen.get(j, -1):
+                seen[j] = rr
+        if not self.virtual:
+            for c in self.local:
+                if c not in self.suppressed:
+                    seen[c] = max(seen[c], max(r for _, r in self.slot_meta[c]))
+        live = [j for j in self.sources if self._last_round - seen[j] <= self.liveness_timeout]
+        if not live:
+            return None
+        T = min(seen[j] for j in live)
+        return T if T > self.applied_T else None
+
+    def _local_sources(self, T: int) -> Dict[int, tuple]:
+        """Hosted clients as sources (not virtual): the send slot of each one's newest post of a
+        round <= T (read in place)."""
+        out = {}
+        if self.virtual:
+            return out
+        from .mailbox import Snapshot
+        for c in self.local:
+            cand = [(s, v, r) for s, (v, r) in enumerate(self.slot_meta[c])
+                    if v > self.applied[c] and r >= 0]
+            if not cand:
+                continue
+            ok = [x for x in cand if x[2] <= T]
+            s_, v, r = max(ok, key=lambda x: x[1]) if ok else min(cand, key=lambda x: x[1])
+            out[c] = (self.send_buf[c][s_], Snapshot(v, r, 0, 0, b""))
+        return out
+
+    @torch.no_grad()
+    def _poll_complete(self, streams, param_out) -> int:
+        tr = self.transport
+        h = self._inflight
+        if h is None:
+            md = getattr(self, "_mix_done", None)
+            remote = [j for j in self.remote_needed]
+            if not remote:   # every source hosted here: the gate decides without a fetch
+                T = self._gate({})
+                return 0 if T is None else self._apply_complete(T, {}, None, streams, param_out)
+            self._inflight = tr.fetch_begin(self._want(remote), self.stage,
+                                            after=self._apply_events + ([md] if md is not None else []),
+                                            gate=self._gate)
+            self._apply_events = []
+            h = self._inflight
+        res = tr.fetch_advance(h, self._hash if self.verify else None)
+        if res is None:
+            return 0
+        self._inflight = None
+        if h.gate_round is None:
+            return 0
+        return self._apply_complete(h.gate_round, res, h, streams, param_out)
+
+    def _verified(self, res, h) -> Dict[int, object]:
+        good = {}
+        for j, snap in res.items():
+            ok = True
+            if self.verify:
+                got = h.roots.get(j) if h is not None else None
+                if got is None:
+                    got = ops.root_bytes(ops.merkle_root_deferred(self.stage[j]))
+                ok = got == snap.root
+            self.records.append({"client": j, "kind": "recv", "version": snap.version,
+                                 "root": snap.root.hex(), "ok": ok, "src_round": snap.round})
+            if not ok:
+                self._reject(j, snap.version)
+                continue
+            good[j] = snap
+        return good
+
+    @torch.no_grad()
+    def _apply_complete(self, T: int, res, h, streams, param_out) -> int:
+        """Apply every source's progress up to round T to every hosted client: model (and its
+        compute-dtype copy), round-start record when its round has begun, then the drift
+        correction's control variates from the same round."""
+        good = self._verified(res, h) if res else {}
+        src = {j: (self.stage[j], snap) for j, snap in good.items()}
+        src.update(self._local_sources(T))
+        n, W = self.numel, self.W_mid
+        cuda = self.transport.is_cuda
+        main = torch.cuda.current_stream(self.device) if cuda else None
+        evs = []
+        for c in self.local:
+            views, ws = [], []
+            for j, (buf, _snap) in src.items():
+                w = float(W[c, j]) * self.apply_scale
+                if w != 0.0:
+                    views += [buf[:n], self.replica[j][:n]]
+                    ws += [w, -w]
+            if not views:
+                continue
+            st = (streams or {}).get(c) if cuda else None
+            cur = st if st is not None else main
+            with (torch.cuda.stream(cur) if cuda else _nullctx()):
+                if cuda and h is not None and h.done_event is not None:
+                    cur.wait_event(h.done_event)
+                ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
+                if c in self._started:
+                    ops.gossip_mix_(self.start[c], views, 1.0, ws)
+                if cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    evs.append(ev)
+        # the applied snapshots become the replicas (remote: buffer swap; hosted: a copy, after
+        # every reader of the old replica)
+        if cuda:
+            for ev in evs:
+                main.wait_event(ev)
+        for j, (buf, snap) in src.items():
+            if j in self.stage and buf is self.stage[j]:
+                self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
+            else:
+                self.replica[j].copy_(buf)
+            self.applied[j] = snap.version
+            self.replica_round[j] = snap.round
+        self.applied_T = T
+        self.applied_mid += len(src)
+        self._refresh_aux(streams, main if cuda else None)
+        return len(src)
+
+    @torch.no_grad()
+    def _refresh_aux(self, streams, main) -> None:
+        """Drift correction from the applied round: d_c = sum_j W_cj c_j^T - c_c^T (the
+        sources' control variates as held in the replicas)."""
+        if self.aux is None or self.aux_sink is None:
+            return
+        n, W = self.numel, self.W_mid
+        done = torch.cuda.Event() if main is not None else None
+        if done is not None:
+            done.record(main)     # the replica copies
+        for c in self.local:
+            views, ws = [], []
+            for j in self.sources:
+                w = float(W[c, j]) - (1.0 if j == c else 0.0)
+                if w != 0.0 and self.applied[j] > 0:
+                    views.append(self.replica[j][n:])
+                    ws.append(w)
+            st = (streams or {}).get(c) if main is not None else None
+            cur = st if st is not None else main
+            with (torch.cuda.stream(cur) if main is not None else _nullctx()):
+                if done is not None:
+                    cur.wait_event(done)
+                self.aux_sink.set_correction(c, views, ws)
+                if main is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    self._apply_events.append(ev)
+
+    @torch.no_grad()
+    def _end_complete(self, round_idx: int, W: np.ndarray, param_out, steps) -> Dict[str, float]:
+        b0 = self.transport.bytes_posted
+        if self._inflight is not None:   # a mid-round fetch: complete and apply it first
+            h, self._inflight = self._inflight, None
+            res = self.transport.fetch_wait(h, self._hash if self.verify else None)
+            if h.gate_round is not None:
+                self._apply_complete(h.gate_round, res, h, None, param_out)
+        self.publish(round_idx, steps)   # start[c] <- u_c (own progress of the round)
+        self._last_round = round_idx
+        for c in self.local:             # own progress waits for its round to complete
+            ops.gossip_mix_(self.states[c], [self.start[c]], 1.0, [-1.0], (param_out or {}).get(c))
+        tr = self.transport
+        md = getattr(self, "_mix_done", None)
+        if self.remote_needed:
+            h = tr.fetch_begin(self._want(self.remote_needed), self.stage,
+                               after=self._apply_events + ([md] if md is not None else []),
+                               gate=self._gate)
+            self._apply_events = []
+            res = tr.fetch_wait(h, self._hash if self.verify else None)
+            if h.gate_round is not None:
+                self._apply_complete(h.gate_round, res, h, None, param_out)
+        else:
+            T = self._gate({})
+            if T is not None:
+                self._apply_complete(T, {}, None, None, param_out)
+        self.torn = tr.torn
+        self.dead = {j for j in self.sources
+                     if j not in self.local and round_idx - self.seen_round[j] > self.liveness_timeout}
+        if tr.is_cuda:
+            self._mix_done = torch.cuda.Event()
+            self._mix_done.record(torch.cuda.current_stream(self.device))
+        lag = float(round_idx - self.applied_T)
+        ages = [round_idx - self.seen_round[j] for j in self.remote_needed if j not in self.dead]
+        return {"mixed": 1.0, "stale_rounds": lag, "stale_max": lag,
+                "post_lag_rounds": float(np.mean(ages)) if ages else 0.0,
+                "applied_round": float(self.applied_T), "wait_s": 0.0,
+                "bytes_sent": float(tr.bytes_posted - b0),
+                "dead_peers": float(len(self.dead)), "torn": float(self.torn),
+                "rejected_msgs": float(self.rejected_msgs)}
+
+    def _remote(self, c: int, j: int) -> bool:
+        """Does client c receive client j's updates through the transport (late)? Hosted
+        neighbours are exact and same-round, except on virtual ranks (every client its own)."""
+        return j != c if self.virtual else j not in self.states
+
+    def _msg(self, j: int, c: Optional[int] = None) -> torch.Tensor:
+        if j in self.states and not (self.virtual and c is not None and j != c):
             return self.send_buf[j][self.version[j] % 2]
         return self.replica[j]
 
@@ -607,12 +861,13 @@ class MailboxGossip:
         """Newest verified model of client j (the model half of its message)."""
         return self._msg(j)[: self.numel]
 
-    def aux_view(self, j: int) -> torch.Tensor:
-        """Newest verified aux state (control variate) of client j, same version as :meth:`view`
-        (delta exchange: a snapshot fetched this round is still in the staging buffer)."""
+    def aux_view(self, j: int, c: Optional[int] = None) -> torch.Tensor:
+        """Newest verified aux state (control variate) of client j as receiver c holds it, same
+        version as :meth:`view` (delta exchange: a snapshot fetched this round is still in the
+        staging buffer)."""
         if j in self._fresh:
             return self.stage[j][self.numel:]
-        return self._msg(j)[self.numel:]
+        return self._msg(j, c)[self.numel:]
 
     @torch.no_grad()
     def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None):
@@ -636,6 +891,7 @@ class MailboxGossip:
                            self.cum[c] if self.exchange == "delta" else self.states[c])
             if self.aux is not None:
                 ops.cast_copy_(buf[self.numel:], self.aux[c])
+            self.slot_meta[c][slot] = (self.version[c], round_idx)
             roots[c] = ops.merkle_root_deferred(buf) if self.verify else None
             if c in self.tamper:  # in-flight corruption AFTER the commitment was computed
                 buf.view(-1)[: min(64, buf.numel())].add_(1.0)
@@ -655,7 +911,7 @@ class MailboxGossip:
         """Fetch every newer complete snapshot (sync: wait for round ``round_idx``), verify its
         Merkle root against the sender's commitment, adopt the good ones."""
         import time as _time
-        want = {j: self.applied[j] for j in self.remote_needed}
+        want = self._want(self.remote_needed)
         tr = self.transport
         fs = tr.fetch_stream  # GPU: the whole receive path runs on the transport's side stream
         after = getattr(self, "_mix_done", None)
@@ -694,7 +950,7 @@ class MailboxGossip:
             self.records.append({"client": j, "kind": "recv", "version": snap.version,
                                  "root": snap.root.hex(), "ok": good, "src_round": snap.round})
             if not good:
-                self.rejected_msgs += 1
+                self._reject(j, snap.version)
                 continue
             if self.exchange == "delta":
                 self._fresh[j] = snap   # applied (S_new - S_applied) by the mix, then swapped
@@ -733,18 +989,19 @@ class MailboxGossip:
             damp[j] = 1.0 / (1.0 + self.stale_decay * max(0, tau - 1))
         own = self.pend if self.pend is not None else self.start
         for c in self.local:
+            a = self.apply_scale
             if self.pend is not None:   # y_c - u_c + W_cc u_c(previous round)
-                views, ws = [self.start[c], self.pend[c]], [-1.0, float(W[c, c])]
+                views, ws = [self.start[c], self.pend[c]], [-1.0, a * float(W[c, c])]
             else:
-                views, ws = [self.start[c]], [-(1.0 - float(W[c, c]))]
+                views, ws = [self.start[c]], [-(1.0 - a * float(W[c, c]))]
             for j in range(self.n):
                 if j == c or W[c, j] == 0.0:
                     continue
-                if j in self.states:
+                if not self._remote(c, j):
                     views.append(own[j])
-                    ws.append(float(W[c, j]))
+                    ws.append(a * float(W[c, j]))
                 elif j in self._fresh:
-                    wj = float(W[c, j]) * damp[j]
+                    wj = a * float(W[c, j]) * damp[j]
                     views += [self.stage[j][:n], self.replica[j][:n]]
                     ws += [wj, -wj]
             for t, wt in ((extra or {}).get(c) or []):
@@ -783,6 +1040,8 @@ class MailboxGossip:
     def end_of_round(self, round_idx: int, W: np.ndarray,
                      param_out: Optional[Dict[int, torch.Tensor]] = None,
                      steps: Optional[Dict[int, int]] = None) -> Dict[str, float]:
+        if self.apply_mode == "complete":
+            return self._end_complete(round_idx, W, param_out, steps)
         b0, w0 = self.transport.bytes_posted, self.wait_s
         if self._inflight is not None:
             # the round's training is done: complete the mid-round fetch before publishing (its
@@ -802,8 +1061,8 @@ class MailboxGossip:
             for c in self.local:
                 nb = [j for j in range(self.n) if j != c and Wl[c, j] != 0.0]
                 age = sum(float(Wl[c, j]) * max(0, round_idx - self.replica_round[j])
-                          for j in nb if j not in self.states)
-                extra[c] = self.aux_sink.begin(c, float(Wl[c, c]), [self.aux_view(j) for j in nb],
+                          for j in nb if self._remote(c, j))
+                extra[c] = self.aux_sink.begin(c, float(Wl[c, c]), [self.aux_view(j, c) for j in nb],
                                                [float(Wl[c, j]) for j in nb], age)
         if self.exchange == "delta":
             # updates are applied once with the topology's weights (a silent neighbour simply
@@ -835,6 +1094,8 @@ class MailboxGossip:
 
     def take_records(self) -> List[dict]:
         out, self.records = self.records, []
+        if self.virtual:   # in-process receipts: nothing crossed a process, nothing to ledger
+            out = [g for g in out if g["kind"] != "recv"]
         return out
 
     def state_dict(self) -> dict:
@@ -851,6 +1112,10 @@ class MailboxGossip:
                 "replica": t(self.replica), "version": dict(self.version), "steps": dict(self.steps),
                 "applied": dict(self.applied), "replica_round": dict(self.replica_round),
                 "dead": sorted(self.dead), "rejected_msgs": self.rejected_msgs,
+                "applied_T": int(self.applied_T), "last_round": int(self._last_round),
+                "rejected_version": {int(k): int(v) for k, v in self.rejected_version.items()},
+                "seen_round": {int(k): int(v) for k, v in self.seen_round.items()},
+                "slot_meta": {int(c): [list(x) for x in m] for c, m in self.slot_meta.items()},
                 "records": _portable_records(self.records)}
 
     def load_state_dict(self, st: dict):
@@ -870,3 +1135,9 @@ class MailboxGossip:
         self.dead = set(int(x) for x in st["dead"])
         self.rejected_msgs = int(st["rejected_msgs"])
         self.records = list(st.get("records", []))
+        self.applied_T = int(st.get("applied_T", -1))
+        self.rejected_version.update({int(k): int(v) for k, v in st.get("rejected_version", {}).items()})
+        self._last_round = int(st.get("last_round", -1))
+        self.seen_round.update({int(k): int(v) for k, v in st.get("seen_round", {}).items()})
+        for c, m in st.get("slot_meta", {}).items():
+            self.slot_meta[int(c)] = [tuple(int(y) for y in x) for x in m]

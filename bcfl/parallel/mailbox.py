@@ -338,10 +338,57 @@ class MailboxTransport:
                 best = (s, _snap(h, s, v))
         return best
 
+    @staticmethod
+    def pick(h: np.ndarray, want_v: int, max_round: Optional[int] = None
+             ) -> Optional[Tuple[int, Snapshot]]:
+        """Slot to fetch from one inbox's header pair: the newest complete version newer than
+        ``want_v``; with ``max_round`` the newest such version posted in a round <= max_round (a
+        round-gated receiver applies every source's round-T post together). A sender already
+        two rounds past ``max_round`` has no such slot left: its oldest newer version is taken."""
+        cands = []
+        for s in (0, 1):
+            v = int(h[s, W_BEGIN])
+            if v > 0 and v == int(h[s, W_END]) and v > want_v:
+                cands.append((s, _snap(h, s, v)))
+        if not cands:
+            return None
+        if max_round is None:
+            return max(cands, key=lambda x: x[1].version)
+        ok = [x for x in cands if x[1].round <= max_round]
+        return max(ok, key=lambda x: x[1].version) if ok else min(cands, key=lambda x: x[1].version)
+
+    @classmethod
+    def _select(cls, h: "AsyncFetch", first: Dict[int, np.ndarray]) -> Dict[int, Tuple[int, Snapshot]]:
+        """Step 1 of every fetch: the round gate (if any) sees the newest complete round of every
+        inbox and returns the round to fetch (``None``: nothing to fetch now), then one slot per
+        inbox is picked."""
+        T = None
+        if h.gate is not None:
+            nr = {}
+            for j, hj in first.items():
+                nw = cls.newest(hj)
+                if nw is not None:
+                    nr[j] = nw[1].round
+            T = h.gate(nr)
+            h.gate_round = T
+            if T is None:
+                return {}
+        picked = {}
+        for j, hj in first.items():
+            nw = cls.pick(hj, h.want[j], T)
+            if nw is not None:
+                picked[j] = nw
+        return picked
+
     def fetch(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
-              after: Optional["torch.cuda.Event"] = None) -> Dict[int, Snapshot]:
+              after: Optional["torch.cuda.Event"] = None, gate=None,
+              handle: Optional["AsyncFetch"] = None) -> Dict[int, Snapshot]:
         """For every inbox j with a complete version newer than ``want[j]``, copy it into
         ``out[j]`` and return the validated snapshots; torn reads are dropped.
+
+        ``gate(newest_rounds: {j: round}) -> Optional[int]``: round-gated fetch — the slot of
+        round <= the returned round is taken (:meth:`pick`); ``None`` fetches nothing. The gate's
+        decision is left in ``handle.gate_round`` when a handle is passed.
 
         GPU: everything runs on :attr:`fetch_stream`, first ordered after ``after`` (the event
         after which the ``out`` buffers are no longer read, e.g. the previous mix); a consumer on
@@ -351,16 +398,15 @@ class MailboxTransport:
         if fs is not None and after is not None:
             fs.wait_event(after)
         first = self.headers(js)
-        picked: Dict[int, Tuple[int, Snapshot]] = {}
-        for j in js:
-            nw = self.newest(first[j])
-            if nw is not None and nw[1].version > want[j]:
-                picked[j] = nw
-                if fs is not None:
-                    with torch.cuda.stream(fs):
-                        out[j].copy_(self.inbox[j].slots[nw[0]], non_blocking=True)
-                else:
-                    out[j].copy_(self.inbox[j].slots[nw[0]])
+        hd = handle if handle is not None else AsyncFetch(want, out)
+        hd.gate = gate
+        picked = self._select(hd, first)
+        for j, nw in picked.items():
+            if fs is not None:
+                with torch.cuda.stream(fs):
+                    out[j].copy_(self.inbox[j].slots[nw[0]], non_blocking=True)
+            else:
+                out[j].copy_(self.inbox[j].slots[nw[0]])
         if not picked:
             return {}
         second = self.headers(list(picked))  # stream-ordered after the payload copies
@@ -415,14 +461,16 @@ class MailboxTransport:
 
     # ---------------------------------------------------------- non-blocking receive
     def fetch_begin(self, want: Dict[int, int], out: Dict[int, torch.Tensor],
-                    after: Sequence["torch.cuda.Event"] = ()) -> "AsyncFetch":
+                    after: Sequence["torch.cuda.Event"] = (), gate=None) -> "AsyncFetch":
         """Start a NON-BLOCKING fetch (GPU): the header read is queued on the fetch stream into
         pinned host memory and nothing waits; :meth:`fetch_advance` moves it on when its event
         has completed. ``after``: events after which the ``out`` buffers are free (their last
-        readers). CPU: completes synchronously (the shared-memory copies are host copies)."""
+        readers); ``gate``: as in :meth:`fetch`. CPU: completes synchronously (the shared-memory
+        copies are host copies)."""
         h = AsyncFetch(want, out)
+        h.gate = gate
         if not self.is_cuda:
-            h.result = self.fetch(want, out)
+            h.result = self.fetch(want, out, gate=gate, handle=h)
             return h
         fs = self.fetch_stream
         for ev in after:
@@ -452,12 +500,8 @@ class MailboxTransport:
             return None
         fs = self.fetch_stream
         if h.step == 1:
-            first = h.hdr.numpy()
-            picked = {}
-            for i, j in enumerate(h.js):
-                nw = self.newest(first[i])
-                if nw is not None and nw[1].version > h.want[j]:
-                    picked[j] = nw
+            hn = h.hdr.numpy()
+            picked = self._select(h, {j: hn[i] for i, j in enumerate(h.js)})
             if not picked:
                 h.result = {}
                 return h.result
@@ -516,6 +560,8 @@ class AsyncFetch:
         self.js: List[int] = []
         self.hdr = self.hdr2 = self.root_host = None
         self.roots: Dict[int, bytes] = {}
+        self.gate = None                  # round gate (MailboxTransport.fetch)
+        self.gate_round: Optional[int] = None
 
     @property
     def done_event(self):

@@ -128,12 +128,61 @@ def _heartbeat(rank: int, what: str, every_s: float = 30.0) -> list:
     return cell
 
 
+MODEL_NAMES = {"bert-base": "BERT-base", "biobert": "BioBERT", "albert-base-v2": "ALBERT-base-v2",
+               "distilbert": "DistilBERT", "llama3-8b-lora": "Llama-3-8B LoRA",
+               "tiny-bert": "tiny-BERT", "tiny-llama-lora": "tiny-Llama LoRA"}
+
+
+def metric_name(cfg) -> str:
+    """BASELINE.json's metric string for the bench's config (the default run names exactly
+    "per-round wall-clock + final accuracy, BERT-base 8-client async P2P Non-IID")."""
+    from bcfl.fl.drift import LABEL_SKEWED
+    mode = ("server FedAvg" if cfg.mode == "server" else
+            "async P2P" if cfg.async_gossip else "sync P2P")
+    part = "Non-IID" if cfg.partition in LABEL_SKEWED else "IID"
+    return (f"per-round wall-clock + final accuracy, {MODEL_NAMES.get(cfg.model, cfg.model)} "
+            f"{cfg.num_clients}-client {mode} {part}")
+
+
+def _protocol(fed, timed) -> dict:
+    """What the round's exchange actually mixed: exchange kind (``state`` =
+    neighbours' model states, ``delta`` = their cumulative updates, each applied once), how it is
+    applied, the transport, the mean staleness of the applied neighbour updates over the timed
+    rounds, and how many received updates were re-hashed and verified against their sender's
+    committed Merkle root."""
+    g = fed.gossip
+    if g is None:
+        return {"exchange": "fedavg", "transport": fed.cfg.server_transport}
+    st = [float(h.get("stale_rounds") or 0.0) for h in timed]
+    verified = 0
+    if fed.ledger is not None:
+        verified = sum(1 for b in fed.ledger.blocks() if b["kind"] == "verify" and b["verdict"] == "accept")
+    out = {"exchange": getattr(g, "exchange", "state"),
+           "apply": (getattr(g, "apply_mode", None) if getattr(g, "exchange", "") == "delta" else None),
+           "transport": fed.transport,
+           "virtual_ranks": bool(getattr(g, "virtual", False)),
+           "mix_staleness_rounds": (sum(st) / len(st)) if st else 0.0,
+           "verified_receives": verified}
+    tr = getattr(g, "transport", None)
+    if hasattr(tr, "stats"):
+        out["loopback"] = tr.stats()
+    return out
+
+
 def _async_mix_desc(fed) -> str:
     g = fed.gossip
     delta = getattr(g, "exchange", "state") == "delta"
+    complete = getattr(g, "apply_mode", "") == "complete"
     d = ("neighbours' cumulative updates applied once each" + (
+        (", every source's round-T update together once the round is complete (own included), "
+         + ("between local steps" if getattr(g, "apply_on_arrival", False) else "at the round end"))
+        if complete else
         ", on arrival between local steps" if getattr(g, "apply_on_arrival", False) else
         ", at the round end") if delta else "newest complete snapshot of each neighbour")
+    if getattr(g, "virtual", False):
+        lag = g.transport.lag
+        d += (f" (in-process virtual ranks: every post visible {lag[0]}-{lag[1]} local steps "
+              "after it was made)")
     lead = int(fed.cfg.gossip_max_lead)
     d += (f"; bounded staleness: waits only while a neighbour is > {lead} rounds behind"
           if lead > 0 and fed.rt.distributed else "; never waits")
@@ -280,7 +329,7 @@ def main():
     fed.finish()
     if rt.is_main:
         rec = {
-            "metric": "per-round wall-clock + final accuracy, BERT-base 8-client async P2P Non-IID",
+            "metric": metric_name(cfg),
             "value": s_per_round,
             "unit": "s/round",
             "n_gpus": rt.world,
@@ -333,7 +382,8 @@ def main():
                        "overlap_wgrad": ops.wgrad_overlap_enabled(),
                        "checkpoint_every_round": cfg.save_every == 1 and ck is not None
                                                  and ck.skipped == 0,
-                       "gossip_transport": fed.transport},
+                       "gossip_transport": fed.transport,
+                       "protocol": _protocol(fed, timed)},
             "checkpoints": {"saved": ck.saved if ck else 0, "skipped": ck.skipped if ck else 0},
             "exchange": exchange,
             "p2p_post_measured": p2p,
