@@ -127,11 +127,15 @@ class FLConfig:
     #                                     made (0 = at once: the round-end collect sees every post)
     gossip_apply_scale: float = 1.0     # delta exchange: fraction of the neighbours' (and own) mean
     #                                     update a model takes in (outer step size; 1 = the mean)
-    gossip_apply: str = "arrival"       # delta exchange: "arrival" = each neighbour's new progress
-    #                                     is applied as soon as it lands | "complete" = the round-T
-    #                                     posts of ALL live sources (own included) are applied
-    #                                     together once the last has landed, so every model holds
-    #                                     complete rounds (no partial-round class tilt)
+    gossip_apply: str = "complete"      # delta exchange: "complete" = the round-T posts of ALL
+    #                                     live sources (own included) are applied together once the
+    #                                     last has landed (mid-round, never waiting), so every model
+    #                                     holds complete rounds — no partial-round class tilt |
+    #                                     "arrival" = each neighbour's new progress is applied as
+    #                                     soon as it lands (round 4). BERT-base, 8 label-shard
+    #                                     clients, post lags 0-12 local steps: complete 0.94-0.996
+    #                                     over 9 runs, arrival 0.50-0.83
+    #                                     (profiles/async_protocol_r5.jsonl)
     verify_updates: bool = True         # receivers re-hash every received payload vs its root
     wire_dtype: str = "bf16"            # dtype on the wire for gossip deltas (bf16 | fp32)
     fedavg_weighting: str = "examples"  # examples | batches (reference Flower quirk) | uniform
@@ -356,11 +360,17 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # (SCAFFOLD control variates, bcfl/fl/drift.py): without it the mixed model collapses to the
     # majority rate after every local epoch. IID partitions train better without it
     # (profiles/accuracy_curves_iid_mi355x.json), hence drift_correction="auto".
+    # Round 5 (asynchronous protocol sweep on MI355X, profiles/async_protocol_r5.jsonl): with
+    # round-complete application of the delta exchange, a 0.75-damped drift correction and lr 4e-5
+    # the 8-client federation learns whatever the post lag (0.97-0.996 after 25 rounds, lags 0-8
+    # local steps); at lr 2e-5 / full correction the same protocol is slower (0.93) and with
+    # mid-round application of partial rounds (round 4) it does not learn under jitter (0.51).
     "baseline3_learnable": dict(mode="serverless", model="bert-base", dataset="imdb", num_labels=2,
                                 num_clients=8, num_rounds=20, partition="label_shards",
-                                train_samples=240, test_samples=60, async_gossip=True, lr=2e-5,
+                                train_samples=240, test_samples=60, async_gossip=True, lr=4e-5,
                                 lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
-                                global_test_samples=1000, drift_correction="auto"),
+                                global_test_samples=1000, drift_correction="auto",
+                                drift_correction_scale=0.75),
     "baseline4_biobert_serverless_noniid_trust": dict(mode="serverless", model="biobert",
                                                       dataset="imdb", num_labels=2, num_clients=8,
                                                       num_rounds=20, partition="label_shards",
@@ -386,8 +396,8 @@ PRESETS: Dict[str, Dict[str, Any]] = {
 
 # The random-init learning protocol of baseline3_learnable applied to BASELINE configs 2 and 4
 # (timing records of those configs carry an accuracy that means something).
-_LEARNABLE = dict(lr=2e-5, lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
-                  global_test_samples=1000, drift_correction="auto")
+_LEARNABLE = dict(lr=4e-5, lr_warmup_steps=24, keep_optimizer_state=False, synthetic_signal=12.0,
+                  global_test_samples=1000, drift_correction="auto", drift_correction_scale=0.75)
 # IID splits (no label skew, no drift correction): the averaged Adam-normalised updates of
 # clients that see different rows partly cancel, so FedAvg's effective step shrinks and 20 rounds
 # from random init stay on the plateau at lr 2e-5 (round 3: serverless 5 clients ended at the

@@ -278,6 +278,9 @@ class Federation:
                     self.drift.stale_compensation = cfg.drift_stale_compensation
                     self.gossip.stale_decay = float(cfg.gossip_stale_decay)
                     self.gossip.apply_scale = float(cfg.gossip_apply_scale)
+                    # the run's last round waits (bounded) for every live peer's last post
+                    self.gossip.final_round = cfg.num_rounds - 1
+                    self.gossip.final_timeout_s = float(cfg.gossip_lead_timeout_s)
                     if cfg.gossip_self_delay == "on" and self.gossip.exchange == "delta":
                         self.gossip.enable_self_delay()
                 except MailboxUnavailable as e:
@@ -1427,6 +1430,7 @@ class Federation:
                 "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
                 "stale_max": info.get("stale_max", 0.0),
                 "wait_s": info.get("wait_s", 0.0) + lead_wait, "lead_wait_s": lead_wait,
+                "final_wait_s": info.get("final_wait_s", 0.0),
                 "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
                 "rejected_msgs": info.get("rejected_msgs", 0.0)}
 
@@ -1578,6 +1582,7 @@ class Federation:
                **{k: res[k] for k in ("mixed", "stale_rounds", "stale_max", "wait_s", "lead_wait_s", "torn",
                                       "rejected_msgs", "absent_ranks", "live_weight",
                                       "view_mismatch", "rejoined_ranks", "epochs_skipped",
+                                      "final_wait_s",
                                       "applied_round", "post_lag_rounds") if k in res},
                "ledger_height": len(self.ledger) if self.ledger else 0,
                "tokens_trained": self.tokens_trained, **self.timer.snapshot()}

@@ -33,6 +33,7 @@ replica — 7 neighbours x (217 MB + 433 MB) ≈ 4.6 GB for BERT-base, ≈ 1.8 G
 """
 from __future__ import annotations
 
+import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -450,6 +451,8 @@ class MailboxGossip:
                 if c not in self.replica:
                     self.replica[c] = z()
         self.apply_scale = 1.0   # delta exchange: fraction of the federation's mean update applied
+        self.final_round: Optional[int] = None   # complete mode: this round closes synchronously
+        self.final_timeout_s = 30.0
         self.applied_T = -1                                  # newest round applied everywhere
         self.seen_round = {j: -1 for j in self.sources}      # newest round each source posted
         self.slot_meta = {c: [(0, -1), (0, -1)] for c in self.local}   # (version, round) per slot
@@ -728,44 +731,72 @@ class MailboxGossip:
             good[j] = snap
         return good
 
+    def _scratch(self, name: str) -> torch.Tensor:
+        t = getattr(self, name, None)
+        if t is None:
+            t = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            setattr(self, name, t)
+        return t
+
     @torch.no_grad()
     def _apply_complete(self, T: int, res, h, streams, param_out) -> int:
         """Apply every source's progress up to round T to every hosted client: model (and its
         compute-dtype copy), round-start record when its round has begun, then the drift
-        correction's control variates from the same round."""
+        correction's control variates from the same round.
+
+        Hosted clients with the same mixing row (every client on a complete graph with average
+        mixing) share one update ``D = sum_j W_cj (S_j^T - S_j^applied)``: it is formed once (one
+        pass over the sources' snapshots) and added to each client's model in one fused pass."""
         good = self._verified(res, h) if res else {}
         src = {j: (self.stage[j], snap) for j, snap in good.items()}
         src.update(self._local_sources(T))
         n, W = self.numel, self.W_mid
         cuda = self.transport.is_cuda
         main = torch.cuda.current_stream(self.device) if cuda else None
-        evs = []
+        if cuda and h is not None and h.done_event is not None:
+            main.wait_event(h.done_event)
+        groups: Dict[tuple, List[int]] = {}
         for c in self.local:
+            row = tuple(float(W[c, j]) * self.apply_scale for j in src)
+            if any(w != 0.0 for w in row):
+                groups.setdefault(row, []).append(c)
+        evs = []
+        for row, cs in groups.items():
             views, ws = [], []
-            for j, (buf, _snap) in src.items():
-                w = float(W[c, j]) * self.apply_scale
+            for (j, (buf, _snap)), w in zip(src.items(), row):
                 if w != 0.0:
                     views += [buf[:n], self.replica[j][:n]]
                     ws += [w, -w]
-            if not views:
-                continue
-            st = (streams or {}).get(c) if cuda else None
-            cur = st if st is not None else main
-            with (torch.cuda.stream(cur) if cuda else _nullctx()):
-                if cuda and h is not None and h.done_event is not None:
-                    cur.wait_event(h.done_event)
-                ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
-                if c in self._started:
-                    ops.gossip_mix_(self.start[c], views, 1.0, ws)
-                if cuda:
-                    ev = torch.cuda.Event()
-                    ev.record(cur)
-                    evs.append(ev)
-        # the applied snapshots become the replicas (remote: buffer swap; hosted: a copy, after
-        # every reader of the old replica)
-        if cuda:
-            for ev in evs:
-                main.wait_event(ev)
+            shared = len(cs) > 1
+            if shared:   # D once, on the current stream (after the fetch)
+                D_ = self._scratch("_delta")
+                ops.gossip_mix_(D_, views, 0.0, ws)
+            ready = torch.cuda.Event() if cuda else None
+            if cuda:
+                ready.record(main)
+            for c in cs:
+                st = (streams or {}).get(c) if cuda else None
+                cur = st if st is not None else main
+                with (torch.cuda.stream(cur) if cuda else _nullctx()):
+                    if cuda and cur is not main:
+                        cur.wait_event(ready)
+                    if shared:
+                        ops.gossip_mix_(self.states[c], [D_], 1.0, [1.0], (param_out or {}).get(c))
+                        if c in self._started:
+                            ops.axpby_(self.start[c], D_, 1.0, 1.0)
+                    else:
+                        ops.gossip_mix_(self.states[c], views, 1.0, ws, (param_out or {}).get(c))
+                        if c in self._started:
+                            ops.gossip_mix_(self.start[c], views, 1.0, ws)
+                    if cuda and cur is not main:
+                        ev = torch.cuda.Event()
+                        ev.record(cur)
+                        evs.append(ev)
+            if cuda:   # the shared D (and the old replicas) are free only after every reader
+                for ev in evs:
+                    main.wait_event(ev)
+                evs = []
+        # the applied snapshots become the replicas (remote: buffer swap; hosted: a copy)
         for j, (buf, snap) in src.items():
             if j in self.stage and buf is self.stage[j]:
                 self.replica[j], self.stage[j] = self.stage[j], self.replica[j]
@@ -776,35 +807,75 @@ class MailboxGossip:
         self.applied_T = T
         self.applied_mid += len(src)
         self._refresh_aux(streams, main if cuda else None)
+        if cuda:   # the next fetch may overwrite stage[] (the old replicas) only after all this
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._apply_events.append(ev)
         return len(src)
 
     @torch.no_grad()
     def _refresh_aux(self, streams, main) -> None:
         """Drift correction from the applied round: d_c = sum_j W_cj c_j^T - c_c^T (the
-        sources' control variates as held in the replicas)."""
+        sources' control variates as held in the replicas); with a shared mixing row the
+        federation's c_hat = sum_j W_cj c_j^T is formed once."""
         if self.aux is None or self.aux_sink is None:
             return
         n, W = self.numel, self.W_mid
-        done = torch.cuda.Event() if main is not None else None
-        if done is not None:
-            done.record(main)     # the replica copies
+        live = [j for j in self.sources if self.applied[j] > 0]
+        groups: Dict[tuple, List[int]] = {}
         for c in self.local:
-            views, ws = [], []
-            for j in self.sources:
-                w = float(W[c, j]) - (1.0 if j == c else 0.0)
-                if w != 0.0 and self.applied[j] > 0:
-                    views.append(self.replica[j][n:])
-                    ws.append(w)
-            st = (streams or {}).get(c) if main is not None else None
-            cur = st if st is not None else main
-            with (torch.cuda.stream(cur) if main is not None else _nullctx()):
-                if done is not None:
-                    cur.wait_event(done)
-                self.aux_sink.set_correction(c, views, ws)
-                if main is not None:
-                    ev = torch.cuda.Event()
-                    ev.record(cur)
-                    self._apply_events.append(ev)
+            groups.setdefault(tuple(float(W[c, j]) for j in live), []).append(c)
+        for row, cs in groups.items():
+            views = [self.replica[j][n:] for j, w in zip(live, row) if w != 0.0]
+            ws = [w for w in row if w != 0.0]
+            shared = len(cs) > 1
+            if shared:
+                chat = self._scratch("_chat")
+                ops.gossip_mix_(chat, views, 0.0, ws)
+            done = torch.cuda.Event() if main is not None else None
+            if done is not None:
+                done.record(main)     # the replica copies (and c_hat)
+            evs = []
+            for c in cs:
+                own = self.replica[c][n:] if c in self.replica and self.applied.get(c, 0) > 0 else None
+                st = (streams or {}).get(c) if main is not None else None
+                cur = st if st is not None else main
+                with (torch.cuda.stream(cur) if main is not None else _nullctx()):
+                    if done is not None and cur is not main:
+                        cur.wait_event(done)
+                    if shared:
+                        vs, wv = [chat], [1.0]
+                    else:
+                        vs, wv = list(views), list(ws)
+                    if own is not None:
+                        vs.append(own)
+                        wv.append(-1.0)
+                    self.aux_sink.set_correction(c, vs, wv)
+                    if main is not None and cur is not main:
+                        ev = torch.cuda.Event()
+                        ev.record(cur)
+                        evs.append(ev)
+            if main is not None:   # c_hat is rewritten by the next group / application
+                for ev in evs:
+                    main.wait_event(ev)
+
+    @torch.no_grad()
+    def _collect_complete(self, param_out) -> Optional[int]:
+        tr = self.transport
+        md = getattr(self, "_mix_done", None)
+        if not self.remote_needed:
+            T = self._gate({})
+            if T is not None:
+                self._apply_complete(T, {}, None, None, param_out)
+            return T
+        h = tr.fetch_begin(self._want(self.remote_needed), self.stage,
+                           after=self._apply_events + ([md] if md is not None else []),
+                           gate=self._gate)
+        self._apply_events = []
+        res = tr.fetch_wait(h, self._hash if self.verify else None)
+        if h.gate_round is not None:
+            self._apply_complete(h.gate_round, res, h, None, param_out)
+        return h.gate_round
 
     @torch.no_grad()
     def _end_complete(self, round_idx: int, W: np.ndarray, param_out, steps) -> Dict[str, float]:
@@ -819,19 +890,19 @@ class MailboxGossip:
         for c in self.local:             # own progress waits for its round to complete
             ops.gossip_mix_(self.states[c], [self.start[c]], 1.0, [-1.0], (param_out or {}).get(c))
         tr = self.transport
-        md = getattr(self, "_mix_done", None)
-        if self.remote_needed:
-            h = tr.fetch_begin(self._want(self.remote_needed), self.stage,
-                               after=self._apply_events + ([md] if md is not None else []),
-                               gate=self._gate)
-            self._apply_events = []
-            res = tr.fetch_wait(h, self._hash if self.verify else None)
-            if h.gate_round is not None:
-                self._apply_complete(h.gate_round, res, h, None, param_out)
-        else:
-            T = self._gate({})
-            if T is not None:
-                self._apply_complete(T, {}, None, None, param_out)
+        self._collect_complete(param_out)
+        t0 = time.perf_counter()
+        waited = 0.0
+        if (self.final_round is not None and round_idx >= self.final_round
+                and self.applied_T < round_idx):
+            # the run's last round closes synchronously: wait (bounded) until every live
+            # source's last post has landed, so the final models hold every trained update
+            while self.applied_T < round_idx and time.perf_counter() - t0 < self.final_timeout_s:
+                if self.virtual:
+                    tr.tick(tr.lag[1] + 1)     # in-process: the in-flight posts land now
+                if self._collect_complete(param_out) is None and not self.virtual:
+                    time.sleep(0.002)
+            waited = time.perf_counter() - t0
         self.torn = tr.torn
         self.dead = {j for j in self.sources
                      if j not in self.local and round_idx - self.seen_round[j] > self.liveness_timeout}
@@ -842,7 +913,7 @@ class MailboxGossip:
         ages = [round_idx - self.seen_round[j] for j in self.remote_needed if j not in self.dead]
         return {"mixed": 1.0, "stale_rounds": lag, "stale_max": lag,
                 "post_lag_rounds": float(np.mean(ages)) if ages else 0.0,
-                "applied_round": float(self.applied_T), "wait_s": 0.0,
+                "applied_round": float(self.applied_T), "wait_s": 0.0, "final_wait_s": waited,
                 "bytes_sent": float(tr.bytes_posted - b0),
                 "dead_peers": float(len(self.dead)), "torn": float(self.torn),
                 "rejected_msgs": float(self.rejected_msgs)}

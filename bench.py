@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--out", default=None)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lanes", type=int, default=0, help="concurrent client lanes per GPU (0 = auto)")
+    ap.add_argument("--transport", default="auto",
+                    help="serverless gossip transport: auto (N > 1: one-sided hipIpc mailboxes; N = 1: "
+                         "loopback = every client its own virtual rank, the multi-rank async protocol "
+                         "in one process) | mailbox | loopback | rccl")
     ap.add_argument("--overlap-wgrad", type=int, default=-1, help="1/0 force, -1 auto")
     ap.add_argument("--anomaly-filter", default=None,
                     help="override the preset's update anomaly filter (none|pagerank|modz|both)")
@@ -227,18 +231,32 @@ def main():
         raise SystemExit(f"bench.py --gpus {a.gpus} but the job has WORLD_SIZE={rt.world}: "
                          "launch one rank per GPU (torch.distributed.run --nproc-per-node N)")
     out = a.out or os.path.join("runs", "bench", f"n{rt.world}")
-    cfg = get_preset(a.preset, model=a.model, num_clients=a.clients,
-                     num_rounds=a.warmup + a.steps, mode=a.mode,
-                     **({} if a.lr is None else {"lr": a.lr}),
-                     async_gossip=not a.sync, ledger=not a.no_ledger,
-                     save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
-                     device=a.device, client_lanes=a.lanes, micro_batches=a.micro_batches,
-                     overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad),
-                     **({"batch_size": a.batch_size} if a.batch_size > 0 else {}),
-                     **({"global_test_samples": a.global_test_samples}
-                        if a.global_test_samples > 0 else {}),
-                     **({"anomaly_filter": a.anomaly_filter} if a.anomaly_filter else {}),
-                     **_overrides(a.set))
+    transport = a.transport
+    if transport == "auto" and a.mode == "serverless" and not a.sync:
+        # N = 1: the 8 clients run the SAME asynchronous protocol as on 8 GPUs (delta exchange,
+        # round-complete application, exchanged control variates), each client its own virtual
+        # rank whose posts reach the others 1-2 local steps late (the round-4
+        # single-process bench mixed same-round states, a synchronous algorithm)
+        transport = "loopback" if rt.world == 1 else "mailbox"
+    lanes = a.lanes
+    if transport == "loopback" and lanes == 0:
+        lanes = a.clients          # one lane (HIP stream) per virtual rank
+    tr_kw = {} if transport == "auto" else {"gossip_transport": transport}
+    kw = dict(model=a.model, num_clients=a.clients, num_rounds=a.warmup + a.steps, mode=a.mode,
+              async_gossip=not a.sync, ledger=not a.no_ledger,
+              save_every=0 if a.no_ckpt else 1, out_dir=out, reference_prints=False,
+              device=a.device, client_lanes=lanes, micro_batches=a.micro_batches,
+              overlap_wgrad=None if a.overlap_wgrad < 0 else bool(a.overlap_wgrad), **tr_kw)
+    if a.lr is not None:
+        kw["lr"] = a.lr
+    if a.batch_size > 0:
+        kw["batch_size"] = a.batch_size
+    if a.global_test_samples > 0:
+        kw["global_test_samples"] = a.global_test_samples
+    if a.anomaly_filter:
+        kw["anomaly_filter"] = a.anomaly_filter
+    kw.update(_overrides(a.set))     # --set wins
+    cfg = get_preset(a.preset, **kw)
     hb = _heartbeat(rt.rank, "building the federation")
     fed = Federation(cfg, verbose=False)
     for r in range(a.warmup):
@@ -295,6 +313,7 @@ def main():
               "stale_max": max([float(h.get("stale_max") or 0.0) for h in timed] or [0.0]),
               "wait_s_total": sum(float(h.get("wait_s") or 0.0) for h in timed),
               "lead_wait_s_total": sum(float(h.get("lead_wait_s") or 0.0) for h in timed),
+              "final_wait_s": sum(float(h.get("final_wait_s") or 0.0) for h in timed),
               "torn": sum(float(h.get("torn") or 0.0) for h in timed),
               "rejected_msgs": sum(float(h.get("rejected_msgs") or 0.0) for h in timed),
               "mixed": sum(float(h.get("mixed") or 0.0) for h in timed),

@@ -1,0 +1,73 @@
+"""In-process virtual ranks (bcfl.parallel.loopback): the multi-rank asynchronous delta protocol
+inside ONE process. Properties: a post is invisible (reads as torn) until its lag has elapsed;
+with every post visible at the round end both delta application modes reduce to the reference's
+synchronous mean of the trained models (serverless_NonIID_IMDB.py:296); with lags the rounds
+land late and, in round-complete mode, every model holds complete rounds only."""
+import numpy as np
+import pytest
+import torch
+
+from bcfl.parallel.loopback import LoopbackTransport
+from bcfl.parallel.mailbox import Snapshot
+
+
+def test_loopback_post_visible_after_lag():
+    tr = LoopbackTransport(8, torch.float32, torch.device("cpu"), [0, 1], lag_steps=(2, 2))
+    x = torch.arange(8, dtype=torch.float32)
+    tr.post(0, x, Snapshot(1, 0, 4, 32, b"\0" * 32))
+    out = {0: torch.zeros(8)}
+    assert tr.fetch({0: 0}, out) == {}                  # still in flight
+    assert tr.newest(tr.headers([0])[0]) is None        # begin != end: torn to a reader
+    tr.tick(2)
+    got = tr.fetch({0: 0}, out)
+    assert got[0].version == 1 and got[0].round == 0 and torch.equal(out[0], x)
+    assert tr.fetch({0: 1}, out) == {}                  # nothing newer than the held version
+    # round gate: the receiver asks for round <= 0 although round 1 is posted too
+    tr.post(0, x + 1, Snapshot(2, 1, 8, 32, b"\0" * 32))
+    tr.tick(2)
+    h = tr.fetch_begin({0: 0}, out, gate=lambda rounds: 0)
+    assert h.gate_round == 0 and h.result[0].version == 1
+    assert torch.equal(out[0], x)
+
+
+def _run(tmp_path, tag, **kw):
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    torch.manual_seed(0)
+    base = dict(mode="serverless", model="tiny-bert", dataset="tiny", num_clients=4, num_rounds=3,
+                train_samples=48, test_samples=16, global_test_samples=32, batch_size=16, lr=1e-3,
+                out_dir=str(tmp_path / tag), partition="label_shards", reference_prints=False,
+                save_every=0, device="cpu", drift_correction="none", wire_dtype="fp32",
+                ledger=False)
+    base.update(kw)
+    fed = Federation(FLConfig(**base), verbose=False)
+    fed.run()
+    return fed
+
+
+@pytest.mark.parametrize("apply", ["complete", "arrival"])
+def test_loopback_lag0_equals_synchronous_mean(tmp_path, apply):
+    """Every post visible at the round end: both application modes give every client the mean of
+    the round's trained models — the round-4 single-process (synchronous) result."""
+    ref = _run(tmp_path, "sync", gossip_transport="mailbox")
+    lb = _run(tmp_path, "lb", gossip_transport="loopback", loopback_lag_steps=[0, 0],
+              gossip_apply=apply)
+    assert lb.gossip.virtual and lb.gossip.exchange == "delta"
+    for c in ref.local_clients:
+        torch.testing.assert_close(lb.client_master[c], ref.client_master[c], atol=2e-6, rtol=0)
+
+
+def test_loopback_complete_mode_holds_complete_rounds(tmp_path):
+    """Posts land a few steps into the next round: with round-complete application every client
+    model is the SAME model (the complete rounds applied so far), the last round closes
+    synchronously (stale 0), and earlier rounds report one round of staleness."""
+    fed = _run(tmp_path, "c", gossip_transport="loopback", loopback_lag_steps=[1, 3],
+               gossip_apply="complete", num_rounds=4)
+    ms = [fed.client_master[c] for c in fed.local_clients]
+    for m in ms[1:]:
+        torch.testing.assert_close(m, ms[0], atol=1e-6, rtol=0)
+    st = [h["stale_rounds"] for h in fed.history]
+    assert st[-1] == 0.0 and max(st[:-1]) == 1.0
+    assert fed.gossip.applied_T == 3
