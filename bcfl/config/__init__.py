@@ -145,6 +145,9 @@ class FLConfig:
                                         # be live) | mailbox (one-sided posts of each rank's partial
                                         # sum; a rank that stops posting is left out and the weights
                                         # re-normalised over the live ranks — Flower accept_failures)
+                                        # | mailbox_rs (one-shot reduce-scatter + all-gather over
+                                        # the mailboxes: each rank owns 1/world of the buffer, each
+                                        # link carries 1/world of the model; dead ranks left out)
     server_timeout_s: float = 120.0     # mailbox server: how long a round waits for a rank's post
     overlap_optimizer: bool = False     # one-lane GPU ranks: per-layer AdamW on a side stream
     #                                     launched from the gradient hooks mid-backward (bitwise;
@@ -215,7 +218,7 @@ class FLConfig:
                    "gossip_transport": ("auto", "mailbox", "rccl", "loopback"),
                    "gossip_apply": ("arrival", "complete"),
                    "server_wire_dtype": ("fp32", "bf16"), "dtype": ("bf16", "fp32"),
-                   "server_transport": ("rccl", "mailbox"),
+                   "server_transport": ("rccl", "mailbox", "mailbox_rs"),
                    "drift_correction": ("none", "scaffold", "auto"), "adam_mode": ("hf", "torch"),
                    "drift_exchange": ("auto", "on", "off"),
                    "gossip_exchange": ("auto", "state", "delta"),
@@ -228,7 +231,7 @@ class FLConfig:
         for k, allowed in choices.items():
             if getattr(self, k) not in allowed:
                 raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")
-        if self.mode == "server" and self.server_transport == "mailbox" and self.anomaly_filter != "none":
+        if self.mode == "server" and self.server_transport != "rccl" and self.anomaly_filter != "none":
             raise ValueError("server_transport='mailbox' aggregates without collectives; the update "
                              "anomaly filter needs the global view (use server_transport='rccl')")
         if self.deterministic and self.async_gossip and self.gossip_transport == "mailbox":

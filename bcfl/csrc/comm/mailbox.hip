@@ -104,8 +104,29 @@ pybind11::bytes ipc_handle(Tensor t) {
   return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
-Tensor ipc_open(const std::string& handle, int64_t nbytes, int64_t device) {
+// Can `device` read and write memory that lives on `peer` (xGMI / PCIe peer-to-peer)? Every
+// mailbox post is a copy issued on the sender's device into the receiver's HBM.
+bool can_access_peer(int64_t device, int64_t peer) {
+  if (device == peer) return true;
+  int n = 0;
+  hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  TORCH_CHECK(device >= 0 && device < n && peer >= 0 && peer < n, "can_access_peer: device ",
+              device, " / peer ", peer, " outside the ", n, " visible devices");
+  int ok = 0;
+  hip_check(hipDeviceCanAccessPeer(&ok, (int)device, (int)peer), "hipDeviceCanAccessPeer");
+  return ok != 0;
+}
+
+// peer_device >= 0: the device that owns the exported allocation; mapping it for use on
+// `device` needs peer access between the two (checked first: without it the lazily enabled peer
+// mapping would fail later, inside a copy)
+Tensor ipc_open(const std::string& handle, int64_t nbytes, int64_t device, int64_t peer_device) {
   TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+  if (peer_device >= 0 && peer_device != device) {
+    TORCH_CHECK(can_access_peer(device, peer_device), "mailbox: device ", device,
+                " has no peer access to device ", peer_device,
+                " (hipDeviceCanAccessPeer = 0: no xGMI / PCIe P2P path)");
+  }
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle.data(), sizeof(h));
   int prev = 0;
@@ -138,7 +159,10 @@ void register_mailbox(pybind11::module& m) {
   m.def("mbox_alloc", &mbox_alloc, "dedicated device allocation (IPC-exportable), zeroed",
         pybind11::arg("nbytes"), pybind11::arg("device"), pybind11::arg("flags") = 3);
   m.def("ipc_handle", &ipc_handle, "hipIpcGetMemHandle of an mbox_alloc tensor");
-  m.def("ipc_open", &ipc_open, "map a peer's mailbox (hipIpcOpenMemHandle) as a uint8 tensor");
+  m.def("ipc_open", &ipc_open, "map a peer's mailbox (hipIpcOpenMemHandle) as a uint8 tensor",
+        pybind11::arg("handle"), pybind11::arg("nbytes"), pybind11::arg("device"),
+        pybind11::arg("peer_device") = -1);
+  m.def("can_access_peer", &can_access_peer, "hipDeviceCanAccessPeer(device, peer)");
   m.def("hdr_store", &hdr_store, "stream-ordered header word store (+ fenced end word)");
 }
 

@@ -228,12 +228,13 @@ class Federation:
                                 and cfg.anomaly_filter == "none" and not cfg.compat_chain)
         # server FedAvg over mailboxes (liveness: a dead rank is left out, weights re-normalised)
         self.server_mbox = None
-        if cfg.mode == "server" and cfg.server_transport == "mailbox":
+        if cfg.mode == "server" and cfg.server_transport in ("mailbox", "mailbox_rs"):
             self.collective_free = True
             if self.rt.distributed:
-                from ..parallel.fedavg import MailboxFedAvg
-                self.server_mbox = MailboxFedAvg(self.flat.numel, self.device,
-                                                 cfg.server_timeout_s, cfg.verify_updates)
+                from ..parallel.fedavg import MailboxFedAvg, MailboxReduceScatterFedAvg
+                cls = MailboxReduceScatterFedAvg if cfg.server_transport == "mailbox_rs" else MailboxFedAvg
+                self.server_mbox = cls(self.flat.numel, self.device, cfg.server_timeout_s,
+                                       cfg.verify_updates)
         self.excluded: List[int] = []
         self.skipped_epochs = 0            # mailbox FedAvg: aggregation epochs this rank missed
         self.final_check: Optional[dict] = None
@@ -1245,7 +1246,9 @@ class Federation:
             extra.update(absent_ranks=absent, live_weight=self._server_live["live_weight"],
                          rejoined_ranks=self._server_live["rejoined_ranks"],
                          view_mismatch=self._server_live["view_mismatch"],
-                         epoch=int(self._server_live.get("epoch", r + 1)), epochs_skipped=sk)
+                         epoch=int(self._server_live.get("epoch", r + 1)), epochs_skipped=sk,
+                         **({"absent_owners": self._server_live["absent_owners"]}
+                            if "absent_owners" in self._server_live else {}))
             if sk:
                 # this rank joined a later aggregation epoch (started late / excluded as slow):
                 # the skipped epochs were aggregated WITHOUT it and are not trained rounds here

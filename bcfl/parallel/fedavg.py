@@ -202,3 +202,195 @@ class MailboxFedAvg:
 
     def close(self):
         self.transport.close()
+
+
+class MailboxReduceScatterFedAvg:
+    """Server FedAvg as a one-shot reduce-scatter + all-gather over the one-sided mailboxes
+    ("the engine issues a direct one-shot reduce-scatter with send/recv over all 7
+    peers"). The flat buffer is cut into ``world`` contiguous shards; rank k OWNS shard k:
+
+    1. every rank posts shard p of its partial sum ``S_r`` (with its weight ``W_r``) into rank p's
+       reduce inbox — one 1/world-sized copy per peer, all concurrently on side streams, so each
+       xGMI link carries 1/world of the model instead of a full copy (MailboxFedAvg posts the whole
+       partial sum to every peer: (world - 1) x the bytes);
+    2. the owner waits (bounded) for shard k of every rank counted live, sums them in rank order
+       and normalises by the live weight: ``G_k = sum_live S_{r,k} / sum_live W_r``;
+    3. the owner posts ``G_k`` (with its live-rank mask in the header's aux word) to every peer's
+       gather inbox, and every rank assembles ``G`` from the owners' shards.
+
+    Liveness: a rank that misses step 2's deadline is left out of that shard's sum (weights
+    re-normalised, Flower accept_failures as in :class:`MailboxFedAvg`) and only checked — not
+    waited on — afterwards until it posts again; an OWNER that misses step 3's deadline leaves its
+    shard undefined for that round, and each rank keeps its own normalised partial ``S_{r,k} / W_r``
+    there (``absent_owners`` in the round info; the final-model check of the federation reports a
+    resulting split). With every rank live the result equals the all-reduce FedAvg up to the fp32
+    summation order.
+    """
+
+    def __init__(self, numel: int, device: torch.device, timeout_s: float = 120.0,
+                 verify: bool = True, rank: Optional[int] = None, world: Optional[int] = None):
+        rt = D.runtime()
+        self.rank = rt.rank if rank is None else rank
+        self.world = rt.world if world is None else world
+        self.peers = [r for r in range(self.world) if r != self.rank]
+        self.numel, self.device = numel, device
+        self.timeout_s = float(timeout_s)
+        self.verify = verify
+        W = self.world
+        self.shard = -(-numel // W)
+        self.shard = -(-self.shard // 64) * 64          # 256-byte aligned shards
+        self.bounds = [(k * self.shard, min(numel, (k + 1) * self.shard)) for k in range(W)]
+        plan = [(self.rank, p) for p in self.peers]
+        # reduce inboxes: "client" id = sending rank; gather inboxes: "client" id = owner rank
+        self.rs = MailboxTransport(self.shard, torch.float32, device, listen=self.peers,
+                                   send_plan=plan, rank=self.rank, world=self.world)
+        self.ag = MailboxTransport(self.shard, torch.float32, device, listen=self.peers,
+                                   send_plan=plan, rank=self.rank, world=self.world)
+        z = lambda: torch.zeros(self.shard * W, dtype=torch.float32, device=device)  # noqa: E731
+        self.send_buf = [z(), z()]                      # padded partial sums (one per slot)
+        zs = lambda: torch.zeros(self.shard, dtype=torch.float32, device=device)  # noqa: E731
+        self.gsend = [zs(), zs()]
+        self.stage_rs = {p: zs() for p in self.peers}
+        self.stage_ag = {p: zs() for p in self.peers}
+        self.dead: set = set()
+        self.records: List[dict] = []
+        self.bytes_posted = 0
+        self.epoch = 0
+        self.prev_live_mask = (1 << W) - 1
+        self._done = None
+
+    def _key(self, v: int, phase: int, who: int) -> int:
+        """Ledger key of one post: every (sender, key) names ONE payload — the reduce posts of a
+        version differ per destination ``who``, the gather post is one (``who`` = -1)."""
+        return (2 * v + phase) * (self.world + 1) + who + 1
+
+    def _post(self, tr, buf: torch.Tensor, snap: Snapshot, dsts, key: int) -> None:
+        root = ops.merkle_root_deferred(buf) if self.verify else None
+        rd = root
+        if rd is not None and not torch.is_tensor(rd):
+            snap.root, rd = bytes(rd), None
+        tr.post_to(self.rank, buf, snap, dsts, rd)
+        self.records.append({"client": -(self.rank + 1), "kind": "update", "version": key,
+                             "root_t": root})
+
+    def _gather(self, tr, want: Dict[int, int], stage: Dict[int, torch.Tensor],
+                need, key) -> Dict[int, Snapshot]:
+        """Bounded wait for version want[p] of every peer in ``need``; others are only checked."""
+        got: Dict[int, Snapshot] = {}
+        t0 = time.perf_counter()
+        after = self._done
+        while True:
+            left = [p for p in need if p not in got]
+            if not left:
+                break
+            got.update(tr.fetch_exact({p: want[p] for p in left}, stage, after=after))
+            after = None
+            if all(p in got for p in need) or time.perf_counter() - t0 > self.timeout_s:
+                break
+            time.sleep(0.0005)
+        rest = [p for p in want if p not in need]
+        if rest:
+            got.update(tr.fetch_exact({p: want[p] for p in rest}, stage))
+        ok = {}
+        if got and self.verify:
+            fs = tr.fetch_stream
+            ctx = torch.cuda.stream(fs) if fs is not None else None
+            if ctx is not None:
+                ctx.__enter__()
+            try:
+                for p in got:
+                    ok[p] = ops.root_bytes(ops.merkle_root_deferred(stage[p])) == got[p].root
+            finally:
+                if ctx is not None:
+                    ctx.__exit__(None, None, None)
+            if fs is not None:
+                torch.cuda.current_stream(self.device).wait_stream(fs)
+        good = {}
+        for p, sn in got.items():
+            g = ok.get(p, True)
+            self.records.append({"client": -(p + 1), "kind": "recv", "version": key(sn.version),
+                                 "root": sn.root.hex(), "ok": g, "src_round": sn.round})
+            if g:
+                good[p] = sn
+        return good
+
+    def reduce(self, r: int, partial: torch.Tensor, w_local: float) -> Tuple[torch.Tensor, Dict]:
+        W, k, n = self.world, self.rank, self.numel
+        v = self.epoch + 1
+        self.epoch = v
+        slot = v % 2
+        b0 = self.rs.bytes_posted + self.ag.bytes_posted
+        t_start = time.perf_counter()
+        # ---- 1. reduce-scatter: shard p of the partial sum to its owner p ----------------------
+        if self.rs.is_cuda:
+            self.rs.wait_slot_free(self.rank, slot)
+        buf = self.send_buf[slot]
+        buf[:n].copy_(partial)
+        for p in self.peers:
+            a, b = p * self.shard, (p + 1) * self.shard
+            self._post(self.rs, buf[a:b], Snapshot(v, r, _f2i(w_local), self.shard * 4, b"\0" * 32,
+                                                   self.prev_live_mask), [p], self._key(v, 0, p))
+        # ---- 2. the owner reduces its shard over the live ranks ------------------------------------
+        need = [p for p in self.peers if p not in self.dead]
+        got = self._gather(self.rs, {p: v for p in self.peers}, self.stage_rs, need,
+                           lambda ver: self._key(ver, 0, k))
+        absent = sorted(p for p in self.peers if p not in got)
+        rejoined = sorted(p for p in self.peers if p in self.dead and p in got)
+        self.dead = set(absent)
+        live = sorted([k] + list(got))
+        a0 = k * self.shard
+        gk = self.gsend[slot]
+        if self.ag.is_cuda:
+            self.ag.wait_slot_free(self.rank, slot)
+        gk.zero_()
+        wsum = 0.0
+        for q in live:
+            src = buf[a0:a0 + self.shard] if q == k else self.stage_rs[q]
+            ops.axpby_(gk, src, 1.0, 1.0)
+            wsum += w_local if q == k else _i2f(got[q].steps)
+        if wsum > 0 and abs(wsum - 1.0) > 1e-12:
+            ops.scale_(gk, 1.0 / wsum)
+        mask = MailboxFedAvg._mask(live)
+        # ---- 3. all-gather: every owner's G shard to every rank ------------------------------------
+        self._post(self.ag, gk, Snapshot(v, r, _f2i(wsum), self.shard * 4, b"\0" * 32, mask),
+                   self.peers, self._key(v, 1, -1))
+        owners = self._gather(self.ag, {p: v for p in self.peers}, self.stage_ag,
+                              [p for p in self.peers], lambda ver: self._key(ver, 1, -1))
+        out = torch.empty_like(partial)
+        absent_owners = []
+        for q in range(W):
+            a, b = self.bounds[q]
+            if b <= a:
+                continue
+            if q == k:
+                out[a:b].copy_(gk[:b - a])
+            elif q in owners:
+                out[a:b].copy_(self.stage_ag[q][:b - a])
+            else:   # owner gone: this rank's own normalised partial for that shard
+                absent_owners.append(q)
+                out[a:b].copy_(partial[a:b])
+                if w_local > 0:
+                    ops.scale_(out[a:b], 1.0 / w_local)
+        mismatch = sorted(q for q, sn in owners.items() if sn.aux != mask)
+        if self.rs.is_cuda:
+            self._done = torch.cuda.Event()
+            self._done.record(torch.cuda.current_stream(self.device))
+        self.prev_live_mask = mask
+        sent = self.rs.bytes_posted + self.ag.bytes_posted - b0
+        self.bytes_posted += sent
+        return out, {"live_ranks": live, "absent_ranks": absent, "live_weight": wsum,
+                     "rejoined_ranks": rejoined, "view_mismatch": mismatch,
+                     "absent_owners": absent_owners, "wait_s": time.perf_counter() - t_start,
+                     "epoch": v, "epochs_skipped": 0, "bytes_sent": float(sent)}
+
+    def take_records(self) -> List[dict]:
+        out, self.records = self.records, []
+        return out
+
+    def drain(self):
+        self.rs.drain()
+        self.ag.drain()
+
+    def close(self):
+        self.rs.close()
+        self.ag.close()

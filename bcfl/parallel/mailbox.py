@@ -86,7 +86,10 @@ class ShmBackend:
         self.owned.append(path)
         return torch.from_file(path, shared=True, size=nbytes, dtype=torch.uint8), path
 
-    def open(self, handle, nbytes: int) -> torch.Tensor:
+    def peer_ok(self, owner_device: int) -> bool:
+        return True
+
+    def open(self, handle, nbytes: int, owner_device: int = -1) -> torch.Tensor:
         return torch.from_file(handle, shared=True, size=nbytes, dtype=torch.uint8)
 
     def hdr_store(self, hdr: torch.Tensor, slot: int, words: Sequence[int], off: int,
@@ -121,8 +124,12 @@ class HipIpcBackend:
         t = self.C.mbox_alloc(int(nbytes), int(self.device.index), 3)
         return t, bytes(self.C.ipc_handle(t))
 
-    def open(self, handle, nbytes: int) -> torch.Tensor:
-        return self.C.ipc_open(handle, int(nbytes), int(self.device.index))
+    def peer_ok(self, owner_device: int) -> bool:
+        """Peer access from this rank's device to the inbox owner's (same device: always)."""
+        return owner_device < 0 or bool(self.C.can_access_peer(int(self.device.index), int(owner_device)))
+
+    def open(self, handle, nbytes: int, owner_device: int = -1) -> torch.Tensor:
+        return self.C.ipc_open(handle, int(nbytes), int(self.device.index), int(owner_device))
 
     def hdr_store(self, hdr: torch.Tensor, slot: int, words: Sequence[int], off: int,
                   end_word: int = -1, end_value: int = 0):
@@ -181,15 +188,21 @@ class MailboxTransport:
                 handles[j] = (hh, ph)
         except Exception as e:  # reported collectively below, never left half-joined
             err = f"rank {self.rank} inbox allocation / export: {e!r}"
-        # start-up handle exchange (with each rank's allocation outcome)
-        table = D.all_gather_object({"handles": handles, "err": err})
+        # start-up handle exchange (with each rank's allocation outcome and device)
+        dev_idx = device.index if self.is_cuda else -1
+        table = D.all_gather_object({"handles": handles, "err": err, "device": dev_idx})
         self.outbox: Dict[int, List[Tuple[int, _Box]]] = {}
         if err is None and not any(t["err"] for t in table):
             try:
                 for c, dst in send_plan:
+                    owner = int(table[dst].get("device", -1))
+                    if not self.backend.peer_ok(owner):
+                        # fail loudly and collectively: every rank falls back together
+                        raise RuntimeError(f"no peer access from device {dev_idx} to device "
+                                           f"{owner} (rank {dst}'s inbox): hipDeviceCanAccessPeer = 0")
                     hh, ph = table[dst]["handles"][c]
-                    box = _Box(self.backend.open(hh, self.hdr_bytes),
-                               self.backend.open(ph, self.pay_bytes), numel, dtype)
+                    box = _Box(self.backend.open(hh, self.hdr_bytes, owner),
+                               self.backend.open(ph, self.pay_bytes, owner), numel, dtype)
                     self.outbox.setdefault(c, []).append((dst, box))
             except Exception as e:
                 err = f"rank {self.rank} peer mapping: {e!r}"
@@ -274,7 +287,9 @@ class MailboxTransport:
                 self.backend.hdr_store(box.hdr, slot, body, W_ROUND, W_END, snap.version)
             self.bytes_posted += self.payload_bytes
         if evs:
-            self.posted[(c, slot)] = evs
+            # extend, not replace: per-destination posts of one version (post_to) each add the
+            # events of their copies, and the slot is free only after all of them
+            self.posted.setdefault((c, slot), []).extend(evs)
 
     def _collect_timings(self):
         keep = []

@@ -386,6 +386,49 @@ def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path):
         assert int(r0["final_split"]) == 1 and int(r1["final_split"]) == 1
 
 
+def test_server_mailbox_reduce_scatter_equals_allreduce_world8(tmp_path):
+    """server FedAvg as a one-shot reduce-scatter + all-gather over the one-sided
+    mailboxes (each of 8 ranks owns 1/8 of the flat buffer; each peer receives 1/8 of the model
+    per phase) reaches the all-reduce's global model on every rank (fp32 summation order only)
+    and every accepted shard matches its sender's committed root in the cross-rank ledger audit."""
+    kw = {"num_clients": 8, "num_rounds": 2, "train_samples": 32, "test_samples": 16,
+          "global_test_samples": 32}
+    a = run_world(_fed_worker, 8, str(tmp_path / "a"), "server", str(tmp_path / "a"), kw)
+    b = run_world(_fed_worker, 8, str(tmp_path / "b"), "server", str(tmp_path / "b"),
+                  {**kw, "server_transport": "mailbox_rs"})
+    for r in range(8):
+        assert torch.equal(b[r]["master"], b[0]["master"])
+    torch.testing.assert_close(b[0]["master"], a[0]["master"], atol=1e-6, rtol=0)
+
+
+def _rs_dead_worker(rank, world, out):
+    from bcfl.fl import Federation
+    fed = Federation(_cfg("server", out, num_clients=3, num_rounds=4, server_transport="mailbox_rs",
+                          server_timeout_s=2.0), verbose=False)
+    rounds = 2 if rank == world - 1 else fed.cfg.num_rounds
+    for r in range(rounds):
+        fed.run_round(r)
+    if rank == world - 1:
+        return {"rounds": torch.tensor(rounds)}
+    fed.finish(audit=False)
+    return {"rounds": torch.tensor(len(fed.history)), "G": fed.global_master.clone(),
+            "live_w": torch.tensor([h["live_weight"] for h in fed.history], dtype=torch.float64),
+            "absent": [list(h.get("absent_ranks", [])) for h in fed.history]}
+
+
+def test_server_mailbox_reduce_scatter_survives_a_dead_rank(tmp_path):
+    """The reduce-scatter path under a rank that stops after round 1: the survivors finish every
+    round, leave it out of their shards' sums (weights re-normalised 1 -> 2/3) and agree on the
+    global model except on the dead owner's shard, where each keeps its own normalised partial."""
+    res = run_world(_rs_dead_worker, 3, str(tmp_path / "d"), str(tmp_path / "d"))
+    assert int(res[2]["rounds"]) == 2
+    for r in res[:2]:
+        assert int(r["rounds"]) == 4 and torch.isfinite(r["G"]).all()
+        assert r["live_w"].tolist()[:2] == pytest.approx([1.0, 1.0])
+        assert r["live_w"].tolist()[2:] == pytest.approx([2 / 3, 2 / 3])
+        assert r["absent"][2:] == [[2], [2]]
+
+
 @pytest.mark.slow
 def test_server_world8_allreduce_equals_mailbox_fedavg(tmp_path):
     """on 8 ranks (one client each, the 8-GPU layout) server FedAvg through the

@@ -154,13 +154,15 @@ def test_mailbox_exited_peer_does_not_stall(tmp_path):
     assert res[0]["dead"].tolist() == [1]
 
 
-def _fallback_worker(rank, world, out):
+def _fallback_worker(rank, world, out, how="open"):
     from bcfl.fl import Federation
     from bcfl.parallel import mailbox as mb
-    if rank == 1:  # this rank cannot map its peers' inboxes
-        def bad_open(self, handle, nbytes):
+    if rank == 1 and how == "open":  # this rank cannot map its peers' inboxes
+        def bad_open(self, handle, nbytes, owner_device=-1):
             raise OSError("simulated hipIpcOpenMemHandle failure")
         mb.ShmBackend.open = bad_open
+    if rank == 1 and how == "peer":  # no xGMI / P2P path from this rank's device to its peers'
+        mb.ShmBackend.peer_ok = lambda self, owner_device: False
     fed = Federation(_cfg(out), verbose=False)
     for r in range(fed.cfg.num_rounds):
         fed.run_round(r)
@@ -170,10 +172,13 @@ def _fallback_worker(rank, world, out):
             "finite": torch.tensor(int(torch.isfinite(fed.flat.master).all()))}
 
 
-def test_mailbox_failure_on_one_rank_falls_back_to_rccl_everywhere(tmp_path):
-    """A mapping failure on ONE rank is agreed collectively: every rank gets MailboxUnavailable
-    and the federation continues on the lock-step RCCL (here gloo) engine instead of hanging."""
-    res = run_world(_fallback_worker, 2, str(tmp_path), str(tmp_path / "fb"))
+@pytest.mark.parametrize("how", ["open", "peer"])
+def test_mailbox_failure_on_one_rank_falls_back_to_rccl_everywhere(tmp_path, how):
+    """A mapping failure on ONE rank — the IPC open itself, or no peer access between the two
+    devices (hipDeviceCanAccessPeer = 0, checked before mapping) — is agreed collectively: every
+    rank gets MailboxUnavailable and the federation continues on the lock-step RCCL (here gloo)
+    engine instead of hanging or failing inside a later copy."""
+    res = run_world(_fallback_worker, 2, str(tmp_path), str(tmp_path / "fb"), how)
     for r in res:
         assert int(r["transport_rccl"]) == 1 and int(r["collective_free"]) == 0
         assert int(r["finite"]) == 1
