@@ -281,7 +281,9 @@ def test_bench_path_world8_anomaly_filter_consensus(tmp_path):
 def _server_liveness_worker(rank, world, out, exit_after):
     from bcfl.fl import Federation
     fed = Federation(_cfg("server", out, num_clients=3, num_rounds=4, server_transport="mailbox",
-                          server_timeout_s=3.0), verbose=False)
+                          # generous: a LIVE rank slowed by a loaded CPU (parallel test workers)
+                          # must not miss the deadline; the dead rank costs one wait, once
+                          server_timeout_s=15.0), verbose=False)
     rounds = exit_after if rank == world - 1 else fed.cfg.num_rounds
     for r in range(rounds):
         fed.run_round(r)
@@ -404,7 +406,7 @@ def test_server_mailbox_reduce_scatter_equals_allreduce_world8(tmp_path):
 def _rs_dead_worker(rank, world, out):
     from bcfl.fl import Federation
     fed = Federation(_cfg("server", out, num_clients=3, num_rounds=4, server_transport="mailbox_rs",
-                          server_timeout_s=2.0), verbose=False)
+                          server_timeout_s=15.0), verbose=False)
     rounds = 2 if rank == world - 1 else fed.cfg.num_rounds
     for r in range(rounds):
         fed.run_round(r)
