@@ -187,6 +187,7 @@ class FLConfig:
     resume: Optional[str] = None
     eval_local: bool = True
     eval_global: bool = True
+    eval_global_every: int = 1          # score the global draw every k-th round (and the last)
     overlap_global_eval: Optional[bool] = None  # score round r's model on a side stream (own
                                           # replica + snapshot) while round r+1 trains; the
                                           # result lands in history[r] one round later (drain()
@@ -394,7 +395,10 @@ PRESETS: Dict[str, Dict[str, Any]] = {
                                                 # baseline3_learnable): with the generator default a
                                                 # random-init frozen base + LoRA stays at the majority
                                                 # rate (tiny Llama, CPU: 0.54 vs 0.94 after 20 rounds)
-                                                synthetic_signal=12.0),
+                                                synthetic_signal=12.0,
+                                                # the 8B model's 1000-row evaluation is ~1/3 of a
+                                                # round: score every 5th round (and the last)
+                                                eval_global_every=5),
 }
 
 # The random-init learning protocol of baseline3_learnable applied to BASELINE configs 2 and 4

@@ -1107,6 +1107,15 @@ class Federation:
                 break
         self.metrics.write({"round": r, "deferred_global_eval": True, **upd})
 
+    def _global_eval_due(self, r: int) -> bool:
+        """Score the global draw this round? Every ``eval_global_every``-th round and always the
+        last one (an 8B model's 1000-row evaluation costs about a third of its round)."""
+        cfg = self.cfg
+        if not cfg.eval_global:
+            return False
+        k = max(1, int(cfg.eval_global_every))
+        return k == 1 or (r + 1) % k == 0 or r >= cfg.num_rounds - 1
+
     def _eval_global(self, r: int) -> EvalResult:
         with self.timer.phase("eval_global"):
             acc = torch.zeros(4, dtype=torch.float64, device=self.device)
@@ -1233,7 +1242,7 @@ class Federation:
                 client_metrics = self._gather_metrics(loc)
         agg = weighted_average([(n_, m) for _, n_, m in client_metrics]) if client_metrics else {}
         ge = None
-        if cfg.eval_global:
+        if self._global_eval_due(r):
             if self.eval_stream is not None:
                 self._launch_eval_global(r)   # the global model, scored beside round r + 1
             else:
@@ -1395,7 +1404,7 @@ class Federation:
             else:
                 self.flat.load_master(self.client_master[c0])
         ge = None
-        if cfg.eval_global:
+        if self._global_eval_due(r):
             if self.eval_stream is not None:
                 self._launch_eval_global(r)   # filed under round r by _resolve_eval
             else:

@@ -464,3 +464,15 @@ def test_outer_optimizer_nesterov_and_heavy_ball():
             o.step(0, got)
             torch.testing.assert_close(got, want, atol=1e-6, rtol=0)
             x = got
+
+
+@pytest.mark.parametrize("mode", ["server", "serverless"])
+def test_global_eval_every_k_rounds_and_the_last(tmp_out, mode):
+    """eval_global_every = 2 over 5 rounds: the global draw is scored after rounds 1, 3 and 4 (the
+    last round always), the other rounds carry no global accuracy."""
+    fed = Federation(_cfg(tmp_out, mode=mode, num_rounds=5, eval_global_every=2, save_every=0),
+                     verbose=False)
+    fed.run()
+    scored = [h["round"] for h in fed.history if h["global_acc"] is not None]
+    assert scored == [1, 3, 4]
+    assert len(fed.global_accuracies) == 3
