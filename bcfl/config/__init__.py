@@ -125,6 +125,8 @@ class FLConfig:
     loopback_lag_steps: List[int] = field(default_factory=lambda: [1, 2])  # [lo, hi]: a post
     #                                     becomes visible U{lo..hi} local-step ticks after it was
     #                                     made (0 = at once: the round-end collect sees every post)
+    loopback_source_lag: Dict[int, int] = field(default_factory=dict)  # client -> extra ticks
+    #                                     on every post of that client (a persistently slow rank)
     gossip_apply_scale: float = 1.0     # delta exchange: fraction of the neighbours' (and own) mean
     #                                     update a model takes in (outer step size; 1 = the mean)
     gossip_apply: str = "complete"      # delta exchange: "complete" = the round-T posts of ALL
@@ -260,6 +262,8 @@ def config_from_dict(d: Dict[str, Any]) -> FLConfig:
     for k in ("inject_slow", "inject_byzantine"):
         if k in d and d[k] is not None:
             d[k] = {int(a): float(b) for a, b in dict(d[k]).items()}
+    if d.get("loopback_source_lag") is not None:
+        d["loopback_source_lag"] = {int(a): int(b) for a, b in dict(d["loopback_source_lag"]).items()}
     return FLConfig(**d)
 
 

@@ -275,6 +275,7 @@ class Federation:
                                                 apply=cfg.gossip_apply if exch == "delta" else "arrival",
                                                 virtual=loopback,
                                                 lag_steps=tuple(cfg.loopback_lag_steps),
+                                                source_lag=cfg.loopback_source_lag,
                                                 seed=cfg.seed)
                     self.drift.stale_compensation = cfg.drift_stale_compensation
                     self.gossip.stale_decay = float(cfg.gossip_stale_decay)

@@ -387,7 +387,8 @@ class MailboxGossip:
                  verify: bool = True, sync_timeout_s: float = 60.0, rank: Optional[int] = None,
                  world: Optional[int] = None, aux: Optional[Dict[int, torch.Tensor]] = None,
                  aux_sink=None, exchange: str = "state", apply: str = "arrival",
-                 virtual: bool = False, lag_steps=(1, 1), seed: int = 0):
+                 virtual: bool = False, lag_steps=(1, 1), seed: int = 0,
+                 source_lag: Optional[Dict[int, int]] = None):
         from .mailbox import MailboxTransport
         rt = D.runtime()
         self.rank = rt.rank if rank is None else rank
@@ -435,7 +436,7 @@ class MailboxGossip:
         if self.virtual:
             from .loopback import LoopbackTransport
             self.transport = LoopbackTransport(self.msg_numel, self.wire_dtype, self.device,
-                                               self.local, lag_steps, seed)
+                                               self.local, lag_steps, seed, source_lag)
         else:
             self.transport = MailboxTransport(self.msg_numel, self.wire_dtype, self.device,
                                               self.remote_needed, send_plan, self.rank, self.world)

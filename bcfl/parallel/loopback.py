@@ -42,13 +42,17 @@ class LoopbackTransport:
     _select = classmethod(MailboxTransport._select.__func__)
 
     def __init__(self, numel: int, dtype: torch.dtype, device: torch.device,
-                 sources: Sequence[int], lag_steps: Tuple[int, int] = (1, 1), seed: int = 0):
+                 sources: Sequence[int], lag_steps: Tuple[int, int] = (1, 1), seed: int = 0,
+                 source_lag: Optional[Dict[int, int]] = None):
         self.numel, self.dtype, self.device = numel, dtype, device
         self.is_cuda = device.type == "cuda"
         lo, hi = int(lag_steps[0]), int(lag_steps[-1])
         if lo < 0 or hi < lo:
             raise ValueError(f"lag_steps must be 0 <= lo <= hi, got {lag_steps}")
         self.lag = (lo, hi)
+        # persistent extra lag of some sources (ticks): a rank that is always slower than the
+        # others (more tokens per step, a busier device) — skewed pacing, not just jitter
+        self.source_lag = {int(k): int(v) for k, v in (source_lag or {}).items()}
         self.rng = np.random.default_rng(seed)
         self.sources = list(sources)
         self.hdr = {j: np.zeros((2, HDR_WORDS), dtype=np.int64) for j in self.sources}
@@ -71,7 +75,7 @@ class LoopbackTransport:
     def post(self, c: int, payload: torch.Tensor, snap: Snapshot,
              root_dev: Optional[torch.Tensor] = None):
         slot = snap.version % 2
-        lag = int(self.rng.integers(self.lag[0], self.lag[1] + 1))
+        lag = int(self.rng.integers(self.lag[0], self.lag[1] + 1)) + self.source_lag.get(c, 0)
         h = self.hdr[c][slot]
         h[:] = 0
         h[W_BEGIN] = h[W_END] = snap.version
