@@ -1075,6 +1075,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bias", &wgrad_bias);
   m.def("gemm8", &gemm8);
   m.def("set_wgrad_kernel", &set_wgrad_kernel);
+  m.def("set_g8_block_rows", &bcfl::set_g8_block_rows,
+        "pin the block rows (128 / 256) of auto-tiled 8-phase GEMM launches; 0 = auto");
   m.def("set_g8_persistent", &bcfl::set_g8_persistent,
         "persistent BM=128 8-phase GEMM grids for launches with more tiles than CUs");
   m.def("linear_dgrad_acc", &linear_dgrad_acc);

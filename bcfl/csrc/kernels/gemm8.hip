@@ -678,6 +678,11 @@ __global__ __launch_bounds__(T8) void g8_kernel(G8Params p) {
 // (The round-3 overlap-test failure first blamed on it was the dy / dres aliasing race fixed in
 // ops._BDALN: scripts/overlap_diag.py showed the same two gradients off with it on and off.)
 bool g8_persist_default = true;
+// block rows pinned by the runtime (0 = choose per launch, g8_auto_bm): client lanes that run
+// concurrently share the chip, so the tile with the best per-FLOP efficiency (256 rows) wins over
+// the one that fills a lone launch's waves (8-lane bench 0.573-0.575 vs 0.583-0.593 s/round,
+// profiles/bench_r5_gemm_ab.json)
+int g8_bm_pinned = 0;
 
 template <int BM, bool ACOL, bool BCOL, bool PERSIST>
 int g8_dispatch_t(const G8Params& p, hipStream_t s, int nwg) {
@@ -755,6 +760,7 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
 }  // namespace
 
 void set_g8_persistent(bool on) { g8_persist_default = on; }
+void set_g8_block_rows(int bm) { g8_bm_pinned = (bm == 128 || bm == 256) ? bm : 0; }
 
 // Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
 // B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers
@@ -810,6 +816,15 @@ int wgrad_g8_bias_parts(int S) { return 2 * S; }
 // predicted time: on the BERT shapes M = 7680 with N = 768 / 2304 this is 128 (90 -> 180 tiles,
 // 270 -> 540), at M = 11264 and on 4096^3 it is 256 (profiles/g8_v1_vs_hipblaslt.json).
 int g8_auto_bm(int M, int N, int splits) {
+  // BCFL_G8_BM=128/256 pins the block rows (A/B runs: with several client lanes sharing the chip
+  // the wave-count argument below no longer holds and the per-FLOP efficiency decides)
+  static const int env_bm = [] {
+    const char* e = std::getenv("BCFL_G8_BM");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 128 || v == 256) ? v : 0;
+  }();
+  if (env_bm) return env_bm;
+  if (g8_bm_pinned) return g8_bm_pinned;
   const int64_t t256 = (int64_t)((M + 255) / 256) * (N / BN8) * splits;
   const int64_t t128 = (int64_t)((M + 127) / 128) * (N / BN8) * splits;
   const double c256 = (double)((t256 + 255) / 256) * 256.0;

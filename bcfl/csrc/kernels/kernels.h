@@ -109,6 +109,7 @@ int wgrad_g8_bias_parts(int S);  // rows of the bias-partial buffer the g8 weigh
 // weight gradient on the 8-phase kernel (gemm8.hip, both operands transposed-read): split count
 // for an M x N x K problem (0 = shape not supported) and the launch (p.S / p.Mc from it)
 int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override = 0);  // slots: 0 = default
+void set_g8_block_rows(int bm);   // 128 / 256 pins the block rows of auto-tiled g8 launches, 0 = auto
 void set_g8_persistent(bool on);  // persistent BM=128 g8 grids (BCFL_G8_PERSIST overrides)
 int launch_wgrad_g8(const WgradParams& p, hipStream_t s);
 

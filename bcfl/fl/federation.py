@@ -168,7 +168,11 @@ class Federation:
         self.outer = OuterOptimizer(cfg.outer_lr, cfg.outer_momentum, cfg.outer_nesterov,
                                     [-1] if cfg.mode == "server" else self.local_clients,
                                     self.flat.numel, self.device)
-        ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else len(self.lanes) <= 1
+        # auto: on when one client trains at a time — except on a CU-masked device (multi-rank
+        # rehearsals on slices of one GPU): the side-stream weight gradients, sized for 256 CUs,
+        # then crowd the slice's 32 CUs (8-rank rehearsal: 3.6-4.1 s/round with, 2.2 s without)
+        ov = cfg.overlap_wgrad if cfg.overlap_wgrad is not None else (
+            len(self.lanes) <= 1 and not os.environ.get("HSA_CU_MASK"))
         if cfg.deterministic:
             ov = False  # the overlapped path's gradients are not bitwise reproducible
         ops.set_wgrad_overlap(bool(ov and self.is_cuda))
@@ -185,6 +189,10 @@ class Federation:
             # weight-gradient grid they crowd out (0.0975 vs 0.1021 s/round, 3 interleaved reps,
             # profiles/g8_persistent_1client_r3.json); BCFL_G8_PERSIST=0/1 overrides
             ops.native().set_g8_persistent(not bool(ov))
+            # concurrent client lanes share the chip: 256-row GEMM tiles (best per FLOP) instead of
+            # the lone-launch wave fit (8-lane bench -2.5 %, profiles/bench_r5_gemm_ab.json)
+            big = self.flat.numel > 1_000_000_000
+            ops.native().set_g8_block_rows(256 if len(self.lanes) > 1 and not big else 0)
         self.global_master: Optional[torch.Tensor] = None
         if cfg.mode == "server":
             self.global_master = self.flat.master.detach().clone()
