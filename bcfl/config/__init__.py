@@ -76,6 +76,9 @@ class FLConfig:
                                         # partitions (label_shards, ref_contiguous, dirichlet),
                                         # none for IID ones
     drift_correction_scale: float = 1.0
+    drift_correction_lag: int = 2       # round-complete async gossip: round r applies the SCAFFOLD
+    #                                     corrections of complete round r - lag on EVERY client
+    #                                     (same-round corrections sum to zero; 0 = newest held)
     outer_lr: float = 1.0               # round-level outer optimizer on the pseudo-gradient
     outer_momentum: float = 0.0         # x_prev - x_agg (fl/outer.py): lr 1 + momentum 0 = the
     outer_nesterov: bool = True         # reference's plain average; momentum > 0 = FedAvgM

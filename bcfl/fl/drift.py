@@ -38,7 +38,9 @@ PUBLISHES it with its model, in the same versioned, Merkle-committed mailbox pay
 
 * round start (``attach``): ``cv_i <- x_i`` (the start model, needed for ``c_i'``);
 * after training (``after_train``): ``c_i' = (x_i - y_i) / L - s * d_i`` — SCAFFOLD option II,
-  the client's mean update direction with the applied correction removed;
+  the client's mean update direction with the applied correction removed (``d_i`` is the
+  correction frozen at the round start, ``attach``: a newer one received mid-round waits for the
+  next round, so the removed term is exactly the applied one);
 * after the exchange (``after_exchange``): ``d_i = sum_j W_ij c_j' - c_i'`` over the newest
   verified snapshots of the neighbours (whatever round they are from) — the stale-exact
   federation control variate, no waiting on any peer.
@@ -49,7 +51,7 @@ the exchange costs one extra bf16 copy of the parameters on the wire per post.
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 
@@ -88,6 +90,33 @@ class DriftCorrection:
         # when set, cv does not keep its own copy (one model-sized copy per round and one
         # apply pass per arrival less)
         self.start_of: Optional[Dict[int, torch.Tensor]] = None
+        # exchange mode: the correction a client's optimizer applies during a round is FROZEN at
+        # the round start (a copy of buf), and exactly that one is removed from its new control
+        # variate. buf keeps receiving the neighbours' newer control variates mid-round (complete
+        # rounds applied between local steps), but they take effect at the next round: with a
+        # correction that changes after a rank-dependent number of steps, c_i' = (x - y) / L -
+        # s d_i no longer removes what was applied, every client's control variate carries its
+        # own error, and on label shards that error is a per-class bias (8 ranks x 1 client on
+        # one MI355X: 5 of 10 runs stayed on the majority plateau, profiles/async_protocol_r5_*)
+        self.active: Dict[int, torch.Tensor] = {}
+        self.used: Dict[int, bool] = {}
+        self._used_t: Dict[int, Optional[torch.Tensor]] = {}
+        # Round-tagged corrections (exchange mode with round-complete gossip): round r's steps
+        # apply d^(r - corr_lag), the correction formed from the control variates of COMPLETE
+        # round r - corr_lag, on every client of the federation alike. SCAFFOLD's corrections sum
+        # to zero over the clients (sum_i (c_hat - c_i) = 0) only when every client applies
+        # the same round's: a client that happens to hold the newest round (the last rank to
+        # finish sees it complete at its round end) and one that does not would apply corrections
+        # of different rounds, and on label shards the non-zero sum is a class bias that the
+        # federation chases round after round (8 ranks x 1 client on 32-CU slices of one MI355X:
+        # majority-rate plateau in 6 of 6 runs; in-process virtual ranks, where every client sees
+        # a round complete at the same local step, never hit it). Two slots per client (rounds
+        # r - 2 in use, r - 1 arriving); the federation makes sure round r - corr_lag has been
+        # applied before round r starts (with bounded staleness it always has been posted).
+        self.corr_lag: Optional[int] = None
+        self.ring: Dict[int, List[torch.Tensor]] = {}
+        self.ring_round: Dict[int, List[int]] = {}
+        self.lag_miss = 0
         if self.enabled:
             for c in self.clients:
                 self.buf[c] = torch.zeros(numel, dtype=torch.float32, device=device)
@@ -108,17 +137,59 @@ class DriftCorrection:
         self.exchange = False
         self.cv = {}
 
-    def attach(self, opt, c: int, start: Optional[torch.Tensor] = None) -> None:
+    def attach(self, opt, c: int, start: Optional[torch.Tensor] = None,
+               round_idx: Optional[int] = None) -> None:
         """Before client ``c``'s local steps: its optimizer applies ``d_c`` (round 0: nothing).
-        Exchange mode: ``start`` (the round-start model) is kept for ``c_c'``."""
+        Exchange mode: ``start`` (the round-start model) is kept for ``c_c'``; with round-tagged
+        corrections (``corr_lag``) round ``round_idx`` applies d^(round_idx - corr_lag)."""
         if not self.enabled:
             return
-        opt.corr = self.buf[c] if self.ready[c] else None
         opt.corr_scale = self.scale
+        if self.exchange and self.corr_lag is not None and round_idx is not None:
+            self._attach_tagged(opt, c, round_idx)
+        elif self.exchange and self.ready[c]:
+            self.used[c] = True
+            a = self.active.get(c)
+            if a is None:
+                a = self.active[c] = torch.empty_like(self.buf[c])
+            a.copy_(self.buf[c])
+            opt.corr = a
+            self._used_t[c] = a
+        else:
+            self.used[c] = bool(self.ready[c])
+            opt.corr = self.buf[c] if self.ready[c] else None
+            self._used_t[c] = opt.corr
         if self.exchange and self.start_of is None:
             if start is None:
                 raise ValueError("exchanged control variates need the round-start model")
             self.cv[c].copy_(start)
+
+    def _attach_tagged(self, opt, c: int, r: int) -> None:
+        target = r - int(self.corr_lag)
+        rounds = self.ring_round.get(c, [])
+        t = None
+        if target >= 0 and target in rounds:
+            t = self.ring[c][rounds.index(target)]     # never rewritten during this round
+        elif target >= 0 and any(x >= 0 for x in rounds):
+            # round `target` never arrived (a dead source's timeout): the nearest older one,
+            # copied, since the slot it sits in may be rewritten while the round runs
+            self.lag_miss += 1
+            older = [x for x in rounds if 0 <= x <= target] or [max(rounds)]
+            src = self.ring[c][rounds.index(max(older))]
+            t = self.active.get(c)
+            if t is None:
+                t = self.active[c] = torch.empty_like(src)
+            t.copy_(src)
+        opt.corr = t
+        self.used[c] = t is not None
+        self._used_t[c] = t
+
+    def correction_round_needed(self, r: int) -> Optional[int]:
+        """Round-tagged mode: the complete round whose corrections round ``r`` applies."""
+        if not (self.enabled and self.exchange and self.corr_lag is not None):
+            return None
+        t = r - int(self.corr_lag)
+        return t if t >= 0 else None
 
     @staticmethod
     def detach(opt) -> None:
@@ -137,8 +208,9 @@ class DriftCorrection:
                                 [1.0 / lr_sum, -1.0 / lr_sum])
             else:
                 ops.axpby_(self.cv[c], trained, -1.0 / lr_sum, 1.0 / lr_sum)
-            if self.ready[c]:
-                ops.axpby_(self.cv[c], self.buf[c], -self.scale, 1.0)
+            used = self._used_t.get(c)
+            if self.used.get(c) and used is not None:   # the correction the steps applied
+                ops.axpby_(self.cv[c], used, -self.scale, 1.0)
             return
         ops.axpby_(self.buf[c], trained, 1.0 / lr_sum, self.scale if self.ready[c] else 0.0)
 
@@ -170,7 +242,9 @@ class DriftCorrection:
         if not mode or mode == "none" or age <= 0 or not self.ready[c]:
             return None
         if mode == "own":
-            return [(self.cv[c], -L * float(age)), (self.buf[c], -L * float(age) * self.scale)]
+            d_used = self._used_t.get(c) if self.used.get(c) else None
+            d_used = d_used if d_used is not None else self.buf[c]
+            return [(self.cv[c], -L * float(age)), (d_used, -L * float(age) * self.scale)]
         if mode == "global":
             d = self.buf[c]
             d.copy_(self.cv[c])
@@ -196,13 +270,22 @@ class DriftCorrection:
         self.ready[c] = True
 
     @torch.no_grad()
-    def set_correction(self, c: int, views: Sequence[torch.Tensor], weights: Sequence[float]) -> None:
+    def set_correction(self, c: int, views: Sequence[torch.Tensor], weights: Sequence[float],
+                       round_idx: Optional[int] = None) -> None:
         """Exchange mode, round-complete gossip (:meth:`bcfl.parallel.gossip.MailboxGossip.
         _refresh_aux`): ``d_c = sum_j w_j c_j`` with every term from the same applied round
-        (the client's own control variate enters with weight ``W_cc - 1``)."""
+        (the client's own control variate enters with weight ``W_cc - 1``); with round-tagged
+        corrections it is filed under that round (two slots per client)."""
         if not (self.enabled and self.exchange):
             return
         d = self.buf[c]
+        if self.corr_lag is not None and round_idx is not None:
+            if c not in self.ring:
+                self.ring[c] = [self.buf[c], torch.zeros_like(self.buf[c])]
+                self.ring_round[c] = [-1, -1]
+            slot = int(round_idx) % 2
+            d = self.ring[c][slot]
+            self.ring_round[c][slot] = int(round_idx)
         d.zero_()
         if views:
             ops.gossip_mix_(d, list(views), 0.0, [float(w) for w in weights])

@@ -247,6 +247,7 @@ class Federation:
         self.skipped_epochs = 0            # mailbox FedAvg: aggregation epochs this rank missed
         self.final_check: Optional[dict] = None
         self._lead_gone: Dict[int, int] = {}   # bounded staleness: neighbours given up on
+        self._round_now: Optional[int] = None  # serverless round being trained (drift tagging)
         self.gossip: Optional[GossipEngine] = None
         if cfg.mode == "serverless" and not cfg.compat_chain:
             if cfg.topology_probe and self.rt.distributed:
@@ -321,6 +322,9 @@ class Federation:
                 # application would fold a neighbour's update into the model before this round's
                 # verdict on it exists (the round-end mix applies verdicted weights only)
                 self.gossip.W_mid = mixing_matrix(self.nbrs, cfg.mixing)
+                if (self.gossip.apply_mode == "complete" and self.drift.exchange
+                        and cfg.drift_correction_lag > 0):
+                    self.drift.corr_lag = int(cfg.drift_correction_lag)
                 self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival
                                                      and cfg.anomaly_filter == "none"
                                                      and not cfg.inject_byzantine)
@@ -522,6 +526,25 @@ class Federation:
             time.sleep(0.003)
         return time.perf_counter() - t0
 
+    def _await_corrections(self, r: int) -> float:
+        """Round-tagged drift correction (``drift_correction_lag``): round r applies the
+        corrections of complete round r - lag on every client alike, so that round must have been
+        applied here before round r starts. With bounded staleness every live source has posted
+        it by now (equal-speed ranks finished it about a round ago), so this is at most one fetch;
+        a source that is gone stops holding it back after ``gossip_lead_timeout_s`` (its round
+        then completes without it, and a missing correction falls back to the newest older one).
+        Returns the seconds waited."""
+        g = self.gossip
+        need = self.drift.correction_round_needed(r)
+        if need is None or not isinstance(g, MailboxGossip) or g.applied_T >= need:
+            return 0.0
+        t0 = time.perf_counter()
+        while g.applied_T < need and time.perf_counter() - t0 < float(self.cfg.gossip_lead_timeout_s):
+            self._gossip_poll()   # in-process virtual ranks: every poll is one tick of the clock
+            if not g.virtual:
+                time.sleep(0.002)
+        return time.perf_counter() - t0
+
     @contextlib.contextmanager
     def _client_rng(self, c: int):
         g = ops.rng.global_rng()
@@ -542,7 +565,7 @@ class Federation:
                     lane.opt.load_state_dict(self.client_opt[c])
                 else:
                     lane.opt.reset()
-                self.drift.attach(lane.opt, c, lane.flat.master)
+                self.drift.attach(lane.opt, c, lane.flat.master, round_idx=r)
                 self._mark_start(c, lane.flat.master)
                 prev = lane.flat.master.detach().clone() if need_prev else None
                 loss_acc = torch.zeros((), dtype=torch.float32, device=self.device)
@@ -925,7 +948,7 @@ class Federation:
         elif not (self.keep_opt and self._single_opt and self._opt_owner == c):
             self.opt.reset()
             self._opt_owner = c
-        self.drift.attach(self.opt, c, self.flat.master)
+        self.drift.attach(self.opt, c, self.flat.master, round_idx=self._round_now)
         self._mark_start(c, self.flat.master)
         ops.rng.global_rng().load_state(self.client_rng[c])
 
@@ -1115,6 +1138,24 @@ class Federation:
                 rec.update(upd)
                 break
         self.metrics.write({"round": r, "deferred_global_eval": True, **upd})
+
+    def _diag(self, r: int) -> None:
+        """``BCFL_DIAG=1``: one stderr line per round and rank on the asynchronous protocol's
+        state — the newest complete round applied, the classifier bias of this rank's first
+        client (a label-sharded federation stuck on the plateau predicts from it), the norms of
+        the client's drift correction and of its own update of the round (host reads: debugging
+        only)."""
+        import sys
+        g, c = self.gossip, self.local_clients[0]
+        m = self.client_master[c] if self.multi else self.flat.master
+        bias = []
+        for name, (o, n, _s) in zip(self.flat.names, self.flat.slots):
+            if name.endswith("classifier_bias") or name.endswith("classifier.bias"):
+                bias = [round(x, 4) for x in m[o:o + n].tolist()]
+        corr = float(self.drift.buf[c].norm()) if self.drift.enabled else 0.0
+        u = float(g.start[c].norm()) if getattr(g, "exchange", "") == "delta" else 0.0
+        print(f"[diag] rank {self.rt.rank} round {r} applied_T {getattr(g, 'applied_T', None)} "
+              f"bias {bias} corr {corr:.4g} u {u:.4g}", file=sys.stderr, flush=True)
 
     def _global_eval_due(self, r: int) -> bool:
         """Score the global draw this round? Every ``eval_global_every``-th round and always the
@@ -1347,6 +1388,8 @@ class Federation:
         self._run_deferred()            # last round's host reads (its kernels have finished)
         self._resolve_eval_local()      # last round's deferred local scores (long finished)
         lead_wait = self._bound_lead(r)
+        self._round_now = r
+        corr_wait = self._await_corrections(r)
         if self.outer.enabled:
             for c in self.local_clients:
                 self.outer.begin(c, self.client_master[c] if self.multi else self.flat.master)
@@ -1396,6 +1439,8 @@ class Federation:
             info = self.gossip.end_of_round(r, W, pout,
                                             steps={c: losses[c]["batches"] for c in losses})
         recs += self._gossip_records(r, recs)
+        if os.environ.get("BCFL_DIAG") and isinstance(self.gossip, MailboxGossip):
+            self._diag(r)
         self.prev_verdicts = v
         for c in self.local_clients:
             self.drift.after_mix(c, self.client_master[c] if self.multi else self.flat.master)
@@ -1450,7 +1495,8 @@ class Federation:
                 "client_metrics": client_metrics, "bytes_sent": info.get("bytes_sent", 0.0),
                 "mixed": info.get("mixed", 0.0), "stale_rounds": info.get("stale_rounds", 0.0),
                 "stale_max": info.get("stale_max", 0.0),
-                "wait_s": info.get("wait_s", 0.0) + lead_wait, "lead_wait_s": lead_wait,
+                "wait_s": info.get("wait_s", 0.0) + lead_wait + corr_wait, "lead_wait_s": lead_wait,
+                "corr_wait_s": corr_wait,
                 "final_wait_s": info.get("final_wait_s", 0.0),
                 "dead_peers": sorted(self.gossip.dead), "torn": info.get("torn", 0.0),
                 "rejected_msgs": info.get("rejected_msgs", 0.0)}

@@ -672,7 +672,10 @@ class MailboxGossip:
         live = [j for j in self.sources if self._last_round - seen[j] <= self.liveness_timeout]
         if not live:
             return None
-        T = min(seen[j] for j in live)
+        # one complete round per application: every round's control variates then form that
+        # round's corrections (round-tagged SCAFFOLD, fl/drift.py), also when a burst of posts
+        # completes several rounds at once (the next poll applies the next one)
+        T = min(min(seen[j] for j in live), self.applied_T + 1)
         return T if T > self.applied_T else None
 
     def _local_sources(self, T: int) -> Dict[int, tuple]:
@@ -851,7 +854,7 @@ class MailboxGossip:
                     if own is not None:
                         vs.append(own)
                         wv.append(-1.0)
-                    self.aux_sink.set_correction(c, vs, wv)
+                    self.aux_sink.set_correction(c, vs, wv, self.applied_T)
                     if main is not None and cur is not main:
                         ev = torch.cuda.Event()
                         ev.record(cur)
@@ -905,8 +908,13 @@ class MailboxGossip:
                     time.sleep(0.002)
             waited = time.perf_counter() - t0
         self.torn = tr.torn
+        # dead: silent for more than liveness_timeout rounds, or posting only versions that fail
+        # verification (a tampering neighbour: nothing of it accepted for that long)
         self.dead = {j for j in self.sources
-                     if j not in self.local and round_idx - self.seen_round[j] > self.liveness_timeout}
+                     if j not in self.local and (
+                         round_idx - self.seen_round[j] > self.liveness_timeout
+                         or (self.rejected_version[j] > self.applied[j]
+                             and round_idx - self.replica_round[j] > self.liveness_timeout))}
         if tr.is_cuda:
             self._mix_done = torch.cuda.Event()
             self._mix_done.record(torch.cuda.current_stream(self.device))

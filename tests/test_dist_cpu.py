@@ -325,8 +325,10 @@ def _server_lagging_worker(rank, world, out, join_after):
     import json as _json
     import time as _time
     from bcfl.fl import Federation
+    # the deadline only has to separate "not started yet" (rank 1 waits on a flag) from a live
+    # rank on a loaded CPU (parallel test workers): 1 s was flaky there, 4 s is not
     fed = Federation(_cfg("server", out, num_clients=2, num_rounds=10, server_transport="mailbox",
-                          server_timeout_s=1.0), verbose=False)
+                          server_timeout_s=4.0), verbose=False)
     go, joined = os.path.join(out, "rank0_alone.flag"), os.path.join(out, "rank1_joined.flag")
 
     def wait_for(path):   # test-only gates on ROUND progress (no wall-clock assumptions)
