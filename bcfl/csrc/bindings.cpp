@@ -575,6 +575,31 @@ void axpby(Tensor y, Tensor x, double a, double b) {
                               y.numel(), stream()), "axpby");
 }
 
+void delta_round_end(Tensor y, Tensor x, Tensor cum, Tensor wire, c10::optional<Tensor> param_out,
+                     c10::optional<Tensor> d, c10::optional<Tensor> cv, double inv_l, double scale) {
+  check_cuda(y, "y");
+  const int64_t n = y.numel();
+  for (const Tensor* t : {&x, &cum}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == n && t->is_contiguous(),
+                "delta_round_end: fp32 buffers of one size");
+  }
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.is_contiguous(), "delta_round_end: fp32 y");
+  const bool has_cv = cv.has_value() && cv->defined();
+  TORCH_CHECK(wire.is_contiguous() && wire.numel() == (has_cv ? 2 * n : n), "delta_round_end: wire size");
+  if (has_cv) TORCH_CHECK(cv->scalar_type() == at::kFloat && cv->numel() == n, "delta_round_end: cv");
+  const bool has_d = d.has_value() && d->defined();
+  if (has_d) TORCH_CHECK(d->scalar_type() == at::kFloat && d->numel() == n, "delta_round_end: d");
+  const bool has_p = param_out.has_value() && param_out->defined() &&
+                     param_out->data_ptr() != y.data_ptr();
+  if (has_p) TORCH_CHECK(param_out->numel() == n, "delta_round_end: param size");
+  check_rc(bcfl::launch_delta_round_end(
+               y.data_ptr<float>(), x.data_ptr<float>(), cum.data_ptr<float>(),
+               has_d ? d->data_ptr<float>() : nullptr, has_cv ? cv->data_ptr<float>() : nullptr,
+               wire.data_ptr(), dt_of(wire), has_p ? param_out->data_ptr() : nullptr,
+               has_p ? dt_of(*param_out) : -1, (float)inv_l, (float)scale, n, stream()),
+           "delta_round_end");
+}
+
 void cast_copy(Tensor dst, Tensor src) {
   check_cuda(dst, "dst");
   check_cuda(src, "src");
@@ -1112,6 +1137,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mix", &mix);
   m.def("axpby", &axpby);
   m.def("cast_copy", &cast_copy);
+  m.def("delta_round_end", &delta_round_end);
   m.def("delta_encode", &delta_encode);
   m.def("block_sketch", &block_sketch);
   m.def("sha256_leaves", &sha256_leaves);

@@ -240,10 +240,12 @@ __global__ __launch_bounds__(EW_THREADS) void mix_kernel(float* __restrict__ mas
   const int64_t nvec = n / 4;  // n is a multiple of 64 (flat buffers are padded)
   for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
        i += (int64_t)gridDim.x * EW_THREADS) {
-    float acc[4];
-    Vec4<float>::load(master + i * 4, acc);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (self_w != 0.f) {  // self_w = 0: master is overwritten, never read (formed sums, d_c)
+      Vec4<float>::load(master + i * 4, acc);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] *= self_w;
+      for (int k = 0; k < 4; ++k) acc[k] *= self_w;
+    }
     for (int j = 0; j < nn; ++j) {
       float v[4];
       if (args.dt[j] == DT_BF16) Vec4<bf16_t>::load((const bf16_t*)args.p[j] + i * 4, v);
@@ -254,6 +256,47 @@ __global__ __launch_bounds__(EW_THREADS) void mix_kernel(float* __restrict__ mas
     Vec4<float>::store(master + i * 4, acc);
     if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, acc);
     if (pout_f) Vec4<float>::store(pout_f + i * 4, acc);
+  }
+}
+
+// Round end of one client under round-complete delta gossip (bcfl/parallel/gossip.py publish),
+// one pass instead of five (u, S, the two wire casts, the own-progress retraction) plus the
+// client's new SCAFFOLD control variate (fl/drift.py after_train, deferred to here):
+//   u = y - x;  S += u;  wire[:n] = S;  [c = (x - y) / L - s d;  cv = c;  wire[n:] = c]
+//   y <- y - u;  param <- y        (the client's own progress waits for its round to complete)
+// Every term is rounded as the separate kernels rounded it (axpby / mix order of operations).
+template <typename TW>
+__global__ __launch_bounds__(EW_THREADS) void delta_round_end_kernel(
+    float* __restrict__ y, const float* __restrict__ x, float* __restrict__ cum,
+    const float* __restrict__ d, float* __restrict__ cv, TW* __restrict__ wire_m,
+    TW* __restrict__ wire_a, bf16_t* __restrict__ pout_bf, float* __restrict__ pout_f,
+    float inv_l, float s, int64_t n) {
+  const int64_t nvec = n / 4;  // n is a multiple of 64 (flat buffers are padded)
+  for (int64_t i = blockIdx.x * (int64_t)EW_THREADS + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * EW_THREADS) {
+    float yv[4], xv[4], sv[4], dv[4] = {0.f, 0.f, 0.f, 0.f}, u[4], c[4];
+    Vec4<float>::load(y + i * 4, yv);
+    Vec4<float>::load(x + i * 4, xv);
+    Vec4<float>::load(cum + i * 4, sv);
+    if (d) Vec4<float>::load(d + i * 4, dv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      u[k] = yv[k] - xv[k];
+      sv[k] = u[k] + sv[k];
+      c[k] = inv_l * xv[k];
+      c[k] = c[k] + (-inv_l) * yv[k];
+      if (d) c[k] = (-s) * dv[k] + c[k];
+      yv[k] = yv[k] + (-1.f) * u[k];
+    }
+    Vec4<float>::store(cum + i * 4, sv);
+    Vec4<TW>::store(wire_m + i * 4, sv);
+    if (cv) {
+      Vec4<float>::store(cv + i * 4, c);
+      Vec4<TW>::store(wire_a + i * 4, c);
+    }
+    Vec4<float>::store(y + i * 4, yv);
+    if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, yv);
+    if (pout_f) Vec4<float>::store(pout_f + i * 4, yv);
   }
 }
 
@@ -648,6 +691,25 @@ int launch_mix(float* master, const void* const* nbrs, const int* nbr_dt, const 
   hipLaunchKernelGGL(mix_kernel, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s, master, a, nn,
                      self_w, param_dt == DT_BF16 ? (bf16_t*)param_out : nullptr,
                      param_dt == DT_F32 ? (float*)param_out : nullptr, n);
+  return 0;
+}
+
+int launch_delta_round_end(float* y, const float* x, float* cum, const float* d, float* cv,
+                           void* wire, int wire_dt, void* param_out, int param_dt, float inv_l,
+                           float scale, int64_t n, hipStream_t s) {
+  if (n % 4) return -2;
+  bf16_t* pb = param_dt == DT_BF16 ? (bf16_t*)param_out : nullptr;
+  float* pf = param_dt == DT_F32 ? (float*)param_out : nullptr;
+  if (wire_dt == DT_BF16)
+    hipLaunchKernelGGL(delta_round_end_kernel<bf16_t>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s,
+                       y, x, cum, d, cv, (bf16_t*)wire, cv ? (bf16_t*)wire + n : nullptr, pb, pf,
+                       inv_l, scale, n);
+  else if (wire_dt == DT_F32)
+    hipLaunchKernelGGL(delta_round_end_kernel<float>, dim3(ew_grid(n / 4)), dim3(EW_THREADS), 0, s,
+                       y, x, cum, d, cv, (float*)wire, cv ? (float*)wire + n : nullptr, pb, pf,
+                       inv_l, scale, n);
+  else
+    return -3;
   return 0;
 }
 

@@ -62,6 +62,9 @@ int launch_rope(const void* x, void* out, const int* pos, const float* cos, cons
                 int64_t rows, int row_stride, int nrot, int d, int inverse, int dt, hipStream_t s);
 int launch_cast_copy(void* dst, int dst_dt, const void* src, int src_dt, int64_t n, hipStream_t s);
 int launch_axpby(float* y, const void* x, int x_dt, float a, float b, int64_t n, hipStream_t s);
+int launch_delta_round_end(float* y, const float* x, float* cum, const float* d, float* cv,
+                           void* wire, int wire_dt, void* param_out, int param_dt, float inv_l,
+                           float scale, int64_t n, hipStream_t s);
 int launch_mix(float* master, const void* const* nbrs, const int* nbr_dt, const float* w, int nn,
                float self_w, void* param_out, int param_dt, int64_t n, hipStream_t s);
 int launch_delta_encode(const float* x, float* ref, void* out, int out_dt, int64_t n,

@@ -114,6 +114,10 @@ class DriftCorrection:
         # r - 2 in use, r - 1 arriving); the federation makes sure round r - corr_lag has been
         # applied before round r starts (with bounded staleness it always has been posted).
         self.corr_lag: Optional[int] = None
+        # round-complete gossip: the new control variate is formed by the gossip's fused round-end
+        # pass (ops.delta_round_end_, from round_end_terms) instead of in after_train
+        self.defer_cv = False
+        self._pend_L: Dict[int, float] = {}
         self.ring: Dict[int, List[torch.Tensor]] = {}
         self.ring_round: Dict[int, List[int]] = {}
         self.lag_miss = 0
@@ -184,6 +188,16 @@ class DriftCorrection:
         self.used[c] = t is not None
         self._used_t[c] = t
 
+    def round_end_terms(self, c: int):
+        """Deferred control variate (``defer_cv``): ``(d, scale, 1 / L)`` for
+        ``c_c' = (x - y) / L - scale * d`` with the correction the round's steps applied (None:
+        none was); ``None`` when client c did not train this round (nothing to form)."""
+        L = self._pend_L.pop(c, 0.0)
+        if not (self.enabled and self.exchange and self.defer_cv) or L <= 0:
+            return None
+        used = self._used_t.get(c) if self.used.get(c) else None
+        return used, self.scale, 1.0 / L
+
     def correction_round_needed(self, r: int) -> Optional[int]:
         """Round-tagged mode: the complete round whose corrections round ``r`` applies."""
         if not (self.enabled and self.exchange and self.corr_lag is not None):
@@ -202,6 +216,9 @@ class DriftCorrection:
         if not self.enabled or lr_sum <= 0:
             return
         self.lr_sum[c] = float(lr_sum)
+        if self.exchange and self.defer_cv:
+            self._pend_L[c] = float(lr_sum)   # formed at the round end (round_end_terms)
+            return
         if self.exchange:
             if self.start_of is not None:   # cv = (x_c - y_c) / L in one pass
                 ops.gossip_mix_(self.cv[c], [self.start_of[c], trained], 0.0,
@@ -286,9 +303,10 @@ class DriftCorrection:
             slot = int(round_idx) % 2
             d = self.ring[c][slot]
             self.ring_round[c][slot] = int(round_idx)
-        d.zero_()
-        if views:
+        if views:   # self weight 0: d is overwritten (the kernel never reads it)
             ops.gossip_mix_(d, list(views), 0.0, [float(w) for w in weights])
+        else:
+            d.zero_()
         self.ready[c] = True
         self.lr_sum.pop(c, None)
 

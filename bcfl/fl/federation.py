@@ -325,6 +325,8 @@ class Federation:
                 if (self.gossip.apply_mode == "complete" and self.drift.exchange
                         and cfg.drift_correction_lag > 0):
                     self.drift.corr_lag = int(cfg.drift_correction_lag)
+                if self.gossip.apply_mode == "complete" and self.drift.exchange:
+                    self.drift.defer_cv = True   # formed in the gossip's fused round-end pass
                 self.gossip.apply_on_arrival &= bool(cfg.gossip_apply_on_arrival
                                                      and cfg.anomaly_filter == "none"
                                                      and not cfg.inject_byzantine)
@@ -1153,9 +1155,9 @@ class Federation:
             if name.endswith("classifier_bias") or name.endswith("classifier.bias"):
                 bias = [round(x, 4) for x in m[o:o + n].tolist()]
         corr = float(self.drift.buf[c].norm()) if self.drift.enabled else 0.0
-        u = float(g.start[c].norm()) if getattr(g, "exchange", "") == "delta" else 0.0
+        cum = float(g.cum[c].norm()) if getattr(g, "exchange", "") == "delta" else 0.0
         print(f"[diag] rank {self.rt.rank} round {r} applied_T {getattr(g, 'applied_T', None)} "
-              f"bias {bias} corr {corr:.4g} u {u:.4g}", file=sys.stderr, flush=True)
+              f"bias {bias} corr {corr:.4g} cum {cum:.4g}", file=sys.stderr, flush=True)
 
     def _global_eval_due(self, r: int) -> bool:
         """Score the global draw this round? Every ``eval_global_every``-th round and always the

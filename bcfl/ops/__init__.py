@@ -8,6 +8,7 @@ from .functional import (bias_dropout_add_layernorm, layernorm, bias_act, varlen
                          linear_after_act, gemm_supported, lora_linear, lora_swiglu_mlp,
                          xent_stats_, ResidualTap)
 from .flat import (adamw_, adamw_multi_, grad_clip_coef, gossip_mix_, weighted_accumulate_, block_sketch, scale_, axpby_,
+                   delta_round_end_,
                    cast_copy_, merkle_root_sha256, merkle_root_deferred, root_bytes,
                    leaf_digests_sha256)
 
@@ -18,5 +19,6 @@ __all__ = [
     "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad", "linear_act", "linear_after_act",
     "gemm_supported", "lora_linear", "lora_swiglu_mlp", "xent_stats_", "ResidualTap",
     "adamw_", "adamw_multi_", "grad_clip_coef", "gossip_mix_", "weighted_accumulate_", "block_sketch", "scale_", "axpby_",
+    "delta_round_end_",
     "cast_copy_", "merkle_root_sha256", "merkle_root_deferred", "root_bytes", "leaf_digests_sha256",
 ]

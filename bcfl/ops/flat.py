@@ -115,6 +115,18 @@ def axpby_(y: torch.Tensor, x: torch.Tensor, a: float, b: float):
     y.mul_(b).add_(x.to(y.dtype), alpha=a)
 
 
+def delta_round_end_(y: torch.Tensor, x: torch.Tensor, cum: torch.Tensor, wire: torch.Tensor,
+                     param_out: Optional[torch.Tensor] = None, d: Optional[torch.Tensor] = None,
+                     cv: Optional[torch.Tensor] = None, inv_l: float = 0.0, scale: float = 0.0):
+    """Round end of one client under round-complete delta gossip, one pass (elementwise.hip):
+    ``u = y - x; cum += u; wire[:n] = cum; [cv = (x - y) inv_l - scale d; wire[n:] = cv];
+    y -= u; param_out = y``."""
+    if use_native(y):
+        native().delta_round_end(y, x, cum, wire, param_out, d, cv, float(inv_l), float(scale))
+        return
+    ref.delta_round_end_(y, x, cum, wire, param_out, d, cv, inv_l, scale)
+
+
 def scale_(x: torch.Tensor, a: float):
     if use_native(x):
         native().axpby(x, x, 0.0, float(a))

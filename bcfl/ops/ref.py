@@ -188,12 +188,30 @@ def weighted_accumulate_(acc: torch.Tensor, x: torch.Tensor, w: float):
 
 def gossip_mix_(master: torch.Tensor, neighbours: Sequence[torch.Tensor], self_w: float,
                 weights: Sequence[float], param_out: Optional[torch.Tensor] = None):
-    acc = master.float() * self_w
+    acc = master.float() * self_w if self_w != 0.0 else torch.zeros_like(master, dtype=torch.float32)
     for t, w in zip(neighbours, weights):
         acc.add_(t.float(), alpha=w)
     master.copy_(acc)
     if param_out is not None and param_out.data_ptr() != master.data_ptr():
         param_out.copy_(master)
+
+
+def delta_round_end_(y, x, cum, wire, param_out=None, d=None, cv=None, inv_l=0.0, scale=0.0):
+    """Reference of the fused round end (same order of operations as the separate passes)."""
+    n = y.numel()
+    u = y - x
+    cum.add_(u)
+    wire[:n].copy_(cum)
+    if cv is not None:
+        c = x * inv_l
+        c = c + (-inv_l) * y
+        if d is not None:
+            c = (-scale) * d + c
+        cv.copy_(c)
+        wire[n:].copy_(c)
+    y.add_(u, alpha=-1.0)
+    if param_out is not None and param_out.data_ptr() != y.data_ptr():
+        param_out.copy_(y)
 
 
 def block_sketch(x: torch.Tensor, dim: int, seed: int = 0x5EED) -> torch.Tensor:

@@ -494,6 +494,8 @@ class MailboxGossip:
         self._started: set = set()
         self.applied_mid = 0
         self.pend: Optional[Dict[int, torch.Tensor]] = None   # see enable_self_delay
+        self._fused: set = set()       # clients whose round end ran as one fused pass
+        self.fuse_round_end = True     # False: the separate passes (tests compare the two)
 
     def enable_self_delay(self) -> None:
         """Delta exchange: this rank's OWN updates (every hosted client's u_c of round r) enter
@@ -889,9 +891,11 @@ class MailboxGossip:
             res = self.transport.fetch_wait(h, self._hash if self.verify else None)
             if h.gate_round is not None:
                 self._apply_complete(h.gate_round, res, h, None, param_out)
-        self.publish(round_idx, steps)   # start[c] <- u_c (own progress of the round)
+        self.publish(round_idx, steps, param_out)   # start[c] <- u_c (own progress of the round)
         self._last_round = round_idx
         for c in self.local:             # own progress waits for its round to complete
+            if c in self._fused:         # (already retracted by the fused round-end pass)
+                continue
             ops.gossip_mix_(self.states[c], [self.start[c]], 1.0, [-1.0], (param_out or {}).get(c))
         tr = self.transport
         self._collect_complete(param_out)
@@ -950,11 +954,29 @@ class MailboxGossip:
         return self._msg(j, c)[self.numel:]
 
     @torch.no_grad()
-    def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None):
+    def _fused_round_end(self, c: int) -> bool:
+        """Round-complete delta exchange: client c's round end runs as ONE pass
+        (ops.delta_round_end_: u, S, wire image, new control variate, own-progress retraction)."""
+        return (self.fuse_round_end and self.exchange == "delta" and self.apply_mode == "complete"
+                and c not in self.suppressed and c not in self.tamper
+                and (self.aux is None or getattr(self.aux_sink, "defer_cv", False)))
+
+    def publish(self, round_idx: int, steps: Optional[Dict[int, int]] = None,
+                param_out: Optional[Dict[int, torch.Tensor]] = None):
         from .mailbox import Snapshot
         roots = {}
+        self._fused = set()
         if self.exchange == "delta":
+            defer = self.aux is not None and getattr(self.aux_sink, "defer_cv", False)
             for c in self.local:   # u_c = y_c - x_c (in place), S_c += u_c
+                if self._fused_round_end(c):
+                    continue
+                terms = self.aux_sink.round_end_terms(c) if defer else None
+                if terms is not None:   # the deferred control variate (x - y) / L - s d
+                    d, sc, inv_l = terms
+                    ops.gossip_mix_(self.aux[c], [self.start[c], self.states[c]], 0.0, [inv_l, -inv_l])
+                    if d is not None:
+                        ops.axpby_(self.aux[c], d, -sc, 1.0)
                 ops.axpby_(self.start[c], self.states[c], 1.0, -1.0)
                 ops.axpby_(self.cum[c], self.start[c], 1.0, 1.0)
             self._started = set()
@@ -967,10 +989,22 @@ class MailboxGossip:
             if self.transport.is_cuda:
                 self.transport.wait_slot_free(c, slot)
             buf = self.send_buf[c][slot]
-            ops.cast_copy_(buf[: self.numel],
-                           self.cum[c] if self.exchange == "delta" else self.states[c])
-            if self.aux is not None:
-                ops.cast_copy_(buf[self.numel:], self.aux[c])
+            if self._fused_round_end(c):
+                terms = self.aux_sink.round_end_terms(c) if self.aux is not None else None
+                d, sc, inv_l = terms if terms is not None else (None, 0.0, 0.0)
+                cv = self.aux[c] if self.aux is not None else None
+                if cv is not None and terms is None:   # untrained client: its cv stands
+                    ops.cast_copy_(buf[self.numel:], cv)
+                    cv = None
+                ops.delta_round_end_(self.states[c], self.start[c], self.cum[c],
+                                     buf if cv is not None else buf[: self.numel],
+                                     (param_out or {}).get(c), d, cv, inv_l, sc)
+                self._fused.add(c)
+            else:
+                ops.cast_copy_(buf[: self.numel],
+                               self.cum[c] if self.exchange == "delta" else self.states[c])
+                if self.aux is not None:
+                    ops.cast_copy_(buf[self.numel:], self.aux[c])
             self.slot_meta[c][slot] = (self.version[c], round_idx)
             roots[c] = ops.merkle_root_deferred(buf) if self.verify else None
             if c in self.tamper:  # in-flight corruption AFTER the commitment was computed

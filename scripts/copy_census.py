@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--model", default="bert-base")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--transport", default="auto", help="gossip transport (loopback = the N=1 bench's)")
+    ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--torch-prof", action="store_true",
                     help="GPU: attribute runtime copy kernels to the ops that issued them")
     a = ap.parse_args()
@@ -105,7 +107,9 @@ def main():
           if torch.is_tensor(o) and o is not a[0] else 0)
     cfg = get_preset("baseline3_learnable", num_clients=a.clients, num_rounds=a.rounds + 1,
                      global_test_samples=125 * a.clients, out_dir="runs/census",
-                     reference_prints=False, model=a.model, device=a.device)
+                     reference_prints=False, model=a.model, device=a.device,
+                     gossip_transport=a.transport,
+                     client_lanes=a.lanes or (a.clients if a.transport == "loopback" else 0))
     fed = Federation(cfg, verbose=False)
     fed.run_round(0)
     fed.drain()

@@ -299,6 +299,37 @@ def test_flat_ops():
     _close(sk, ref.block_sketch(x.cpu(), 4096).to(DEV), 1e-3, 1e-4)
 
 
+@pytest.mark.parametrize("wire", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("with_cv,with_d", [(True, True), (True, False), (False, False)])
+def test_delta_round_end_matches_reference(wire, with_cv, with_d):
+    """Fused round end of the round-complete gossip (elementwise.hip delta_round_end_kernel) vs
+    the fp32 reference: own update u = y - x, cumulative sum, wire image, control variate
+    (x - y) / L - s d, own-progress retraction and the bf16 parameter copy."""
+    torch.manual_seed(1)
+    n = (1 << 18) + 64
+    y, x, cum = (torch.randn(n, device=DEV) for _ in range(3))
+    d = torch.randn(n, device=DEV) if with_d else None
+    cv = torch.zeros(n, device=DEV) if with_cv else None
+    wire_t = torch.zeros(2 * n if with_cv else n, device=DEV, dtype=wire)
+    po = torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+    ry, rx, rc = y.cpu(), x.cpu(), cum.cpu()
+    rcv = torch.zeros(n) if with_cv else None
+    rwire = torch.zeros(wire_t.numel())
+    rpo = torch.zeros(n)
+    ops.delta_round_end_(y, x, cum, wire_t, po, d, cv, 1.0 / 3.5e-4, 0.75)
+    ref.delta_round_end_(ry, rx, rc, rwire, rpo, d.cpu() if with_d else None, rcv, 1.0 / 3.5e-4, 0.75)
+    torch.cuda.synchronize()
+    _close(y, ry.to(DEV), 1e-6, 1e-6)
+    _close(cum, rc.to(DEV), 1e-6, 1e-6)
+    # the wire's aux half carries c ~ 1e3 (x / L): fp32 agrees to an ulp or two (FMA contraction)
+    atol, rtol = (1e-2, 1e-2) if wire == torch.bfloat16 else (1e-2, 1e-5)
+    _close(wire_t, rwire.to(DEV, wire), atol, rtol)
+    _close(po, ry.to(DEV), 2e-2)
+    if with_cv:
+        _close(cv, rcv.to(DEV), 1e-2, 1e-5)
+    assert torch.equal(x.cpu(), rx)   # the round-start record is only read
+
+
 @pytest.mark.parametrize("nbytes", [4 * 1000, 4096 * 37 + 1024, 1 << 22])
 def test_sha256_merkle_matches_hashlib(nbytes):
     g = torch.Generator().manual_seed(0)

@@ -71,3 +71,30 @@ def test_loopback_complete_mode_holds_complete_rounds(tmp_path):
     st = [h["stale_rounds"] for h in fed.history]
     assert st[-1] == 0.0 and max(st[:-1]) == 1.0
     assert fed.gossip.applied_T == 3
+
+
+def test_fused_round_end_matches_separate_passes(tmp_path):
+    """The round end of the round-complete protocol as ONE pass (ops.delta_round_end_: own update,
+    cumulative sum, wire image, new SCAFFOLD control variate, own-progress retraction) gives the
+    models, cumulative sums and control variates of the separate passes."""
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    kw = dict(mode="serverless", model="tiny-bert", dataset="tiny", num_clients=4, num_rounds=4,
+              train_samples=48, test_samples=16, global_test_samples=32, batch_size=16, lr=1e-3,
+              partition="label_shards", reference_prints=False, save_every=0, device="cpu",
+              drift_correction="scaffold", drift_correction_scale=0.75, ledger=False,
+              gossip_transport="loopback", loopback_lag_steps=[1, 2])
+    feds = []
+    for tag, fuse in (("fused", True), ("sep", False)):
+        fed = Federation(FLConfig(out_dir=str(tmp_path / tag), **kw), verbose=False)
+        fed.gossip.fuse_round_end = fuse   # (the unfused path forms the control variates itself)
+        fed.run()
+        feds.append(fed)
+    a, b = feds
+    assert a.drift.defer_cv and a.gossip._fused and not b.gossip._fused
+    # the same values up to fp32 rounding (the fused pass rounds each term as the separate
+    # kernels do, but the CPU references may contract differently; 4 rounds of Adam amplify it)
+    for c in a.local_clients:
+        torch.testing.assert_close(a.client_master[c], b.client_master[c], atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(a.gossip.cum[c], b.gossip.cum[c], atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(a.drift.cv[c], b.drift.cv[c], atol=1e-3, rtol=1e-4)
