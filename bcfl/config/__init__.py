@@ -110,9 +110,10 @@ class FLConfig:
     gossip_max_lead: int = 1            # async mailbox gossip: bounded staleness (SSP) — do not
     #                                     start a round while a live neighbour's newest applied
     #                                     update is > this many rounds behind (0 = unbounded).
-    #                                     8 ranks on equal CU slices of one MI355X: 1 learns
-    #                                     (0.73 / 0.95 / 0.77 / 0.91 / 0.88), 2 does not (0.50 / 0.50 / 0.69);
-    #                                     profiles/multirank_cu_split_r4.json
+    #                                     With round-complete application and round-tagged
+    #                                     corrections 8 ranks on equal CU slices of one MI355X
+    #                                     never wait (0.958-0.993 over 5 runs,
+    #                                     profiles/async_protocol_r5_cu8_tagged.json)
     gossip_lead_timeout_s: float = 5.0  # ... a neighbour still behind after this counts as dead
     gossip_self_delay: str = "off"      # delta exchange, async: "on" applies this rank's OWN
     #                                     updates one round late, at the mix where the neighbours'
