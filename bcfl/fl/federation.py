@@ -540,6 +540,10 @@ class Federation:
         need = self.drift.correction_round_needed(r)
         if need is None or not isinstance(g, MailboxGossip) or g.applied_T >= need:
             return 0.0
+        if int(self.cfg.gossip_max_lead) <= 0 and self.rt.distributed:
+            # unbounded staleness was asked for: never wait; a client whose round r - lag has not
+            # completed applies the newest older correction it holds (drift.lag_miss counts it)
+            return 0.0
         t0 = time.perf_counter()
         while g.applied_T < need and time.perf_counter() - t0 < float(self.cfg.gossip_lead_timeout_s):
             self._gossip_poll()   # in-process virtual ranks: every poll is one tick of the clock
@@ -1465,15 +1469,15 @@ class Federation:
                 self._launch_eval_global(r)   # filed under round r by _resolve_eval
             else:
                 ge = self._eval_global(r)
-        loc = []
-        for c, t in local_eval.items():
-            a = t.cpu().tolist()
-            e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
-            loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
-        client_metrics = self._gather_metrics(loc) if cfg.eval_local else []
-        if self.verbose and cfg.reference_prints:
-            for c, _, m in sorted(client_metrics):
-                print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
+        host_deferred = self.collective_free and self.is_cuda and not self.rt.distributed
+        client_metrics = []
+        if host_deferred and local_eval:
+            # the lanes' local scores are read at the next round's start with the other deferred
+            # host reads (a read here would idle the GPU from the round's last kernel until the
+            # next round's first launch)
+            self._defer(lambda r=r, le=dict(local_eval): self._file_local_eval(r, le))
+        else:
+            client_metrics = self._local_metrics(local_eval)
         ledger_extra = {"kind": "mix", "rejected": sorted(v.rejected),
                         "stale_rounds": info.get("stale_rounds", 0.0),
                         "dead_peers": sorted(self.gossip.dead)}
@@ -1513,6 +1517,31 @@ class Federation:
         fns, self._deferred = getattr(self, "_deferred", []), []
         for fn in fns:
             fn()
+
+    def _local_metrics(self, local_eval: Dict[int, torch.Tensor]) -> list:
+        """Device [correct, count, loss_sum, batch_mean_sum] per client -> the reference's
+        per-client metrics (gathered across ranks when not collective-free), printed like it."""
+        cfg = self.cfg
+        loc = []
+        for c, t in local_eval.items():
+            a = t.cpu().tolist()
+            e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
+            loc.append((c, e.count, {"accuracy": e.accuracy, "loss": e.ref_loss if cfg.compat_bad_test_loss else e.loss}))
+        client_metrics = self._gather_metrics(loc) if cfg.eval_local else []
+        if self.verbose and cfg.reference_prints:
+            for c, _, m in sorted(client_metrics):
+                print("local_accuracy" + " :" + str(m["accuracy"]), flush=True)
+        return client_metrics
+
+    def _file_local_eval(self, r: int, local_eval: Dict[int, torch.Tensor]) -> None:
+        """Deferred host read of round r's local scores (collective-free single-process runs)."""
+        cm = self._local_metrics(local_eval)
+        for c, n_, m in cm:
+            self.metrics.write({"round": r, "client": c, "local_acc": m.get("accuracy"),
+                                "local_loss": m.get("loss"), "examples": n_})
+        agg = weighted_average([(n_, m) for _, n_, m in cm]) if cm else {}
+        self._patch_history(r, distributed_acc=agg.get("accuracy"),
+                            distributed_loss=agg.get("loss"))
 
     def _patch_history(self, r: int, **kw) -> None:
         for rec in reversed(self.history):

@@ -239,8 +239,10 @@ def main():
         # single-process bench mixed same-round states, a synchronous algorithm)
         transport = "loopback" if rt.world == 1 else "mailbox"
     lanes = a.lanes
-    if transport == "loopback" and lanes == 0:
-        lanes = a.clients          # one lane (HIP stream) per virtual rank
+    if transport == "loopback" and lanes == 0 and "8b" not in a.model.lower():
+        # one lane (HIP stream) per virtual rank; an 8B model keeps the federation's activation-
+        # memory cap (2 lanes: ~45 GB of saved activations per lane at batch 32)
+        lanes = a.clients
     tr_kw = {} if transport == "auto" else {"gossip_transport": transport}
     kw = dict(model=a.model, num_clients=a.clients, num_rounds=a.warmup + a.steps, mode=a.mode,
               async_gossip=not a.sync, ledger=not a.no_ledger,

@@ -10,7 +10,10 @@ import bcfl  # noqa: F401
 from bcfl.config import get_preset
 from bcfl.fl import Federation
 
-cfg = get_preset("baseline3_learnable", save_every=1, out_dir="runs/eager", reference_prints=False)
+# the N = 1 bench's federation: 8 clients as in-process virtual ranks, one lane each
+cfg = get_preset("baseline3_learnable", save_every=1, out_dir="runs/eager", reference_prints=False,
+                 gossip_transport=sys.argv[1] if len(sys.argv) > 1 else "loopback",
+                 client_lanes=8)
 fed = Federation(cfg, verbose=False)
 for r in range(2):
     fed.run_round(r)

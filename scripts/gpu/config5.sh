@@ -7,7 +7,7 @@ mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "lora or skinny or rmsnorm or swiglu or pack" > $OUT/pytest.log 2>&1; rc=$?
 tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || { echo "pytest rc=$rc"; grep -E "Error|assert" $OUT/pytest.log | head -20; exit 1; }
-timeout -k 10 600 python -u bench.py --preset baseline5_llama3_8b_lora_serverless --model llama3-8b-lora --steps ${STEPS:-8} --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
+timeout -k 10 ${BENCH_TIMEOUT:-600} python -u bench.py --preset baseline5_llama3_8b_lora_serverless --model llama3-8b-lora --steps ${STEPS:-8} --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
 python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/bench.json') if l.startswith('{')][-1])

@@ -377,7 +377,9 @@ def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path):
     r0, r1 = res
     assert r0["absent"][0] == [1]                      # rank 0 timed out on the late rank 1
     assert r1["absent"][0] == []                       # ... which joined rank 0's epoch
-    assert r1["skipped"][0] >= 3 and sum(r0["skipped"]) == 0   # the jump is on record
+    # the jump is on record (rank 0 aggregated >= 2 epochs alone before rank 1's first post; how
+    # many exactly depends on how long rank 1 takes to start)
+    assert r1["skipped"][0] >= 2 and sum(r0["skipped"]) == 0
     assert int(r1["rounds_run"]) < int(r0["rounds_run"])        # ... and not run as rounds
     assert any(m for m in r0["mismatch"] + r1["mismatch"])   # the split is reported
     assert r0["absent"][-1] == [] and r1["absent"][-1] == []  # rank 1 came back
