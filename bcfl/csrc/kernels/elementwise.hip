@@ -263,7 +263,8 @@ __global__ __launch_bounds__(EW_THREADS) void mix_kernel(float* __restrict__ mas
 // one pass instead of five (u, S, the two wire casts, the own-progress retraction) plus the
 // client's new SCAFFOLD control variate (fl/drift.py after_train, deferred to here):
 //   u = y - x;  S += u;  wire[:n] = S;  [c = (x - y) / L - s d;  cv = c;  wire[n:] = c]
-//   y <- y - u;  param <- y        (the client's own progress waits for its round to complete)
+//   y <- x;  param <- x            (the client's own progress waits for its round to complete:
+//                                   the model IS its round-start record again, bit for bit)
 // Every term is rounded as the separate kernels rounded it (axpby / mix order of operations).
 template <typename TW>
 __global__ __launch_bounds__(EW_THREADS) void delta_round_end_kernel(
@@ -286,7 +287,6 @@ __global__ __launch_bounds__(EW_THREADS) void delta_round_end_kernel(
       c[k] = inv_l * xv[k];
       c[k] = c[k] + (-inv_l) * yv[k];
       if (d) c[k] = (-s) * dv[k] + c[k];
-      yv[k] = yv[k] + (-1.f) * u[k];
     }
     Vec4<float>::store(cum + i * 4, sv);
     Vec4<TW>::store(wire_m + i * 4, sv);
@@ -294,9 +294,9 @@ __global__ __launch_bounds__(EW_THREADS) void delta_round_end_kernel(
       Vec4<float>::store(cv + i * 4, c);
       Vec4<TW>::store(wire_a + i * 4, c);
     }
-    Vec4<float>::store(y + i * 4, yv);
-    if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, yv);
-    if (pout_f) Vec4<float>::store(pout_f + i * 4, yv);
+    Vec4<float>::store(y + i * 4, xv);
+    if (pout_bf) Vec4<bf16_t>::store(pout_bf + i * 4, xv);
+    if (pout_f) Vec4<float>::store(pout_f + i * 4, xv);
   }
 }
 

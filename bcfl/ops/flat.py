@@ -120,7 +120,7 @@ def delta_round_end_(y: torch.Tensor, x: torch.Tensor, cum: torch.Tensor, wire: 
                      cv: Optional[torch.Tensor] = None, inv_l: float = 0.0, scale: float = 0.0):
     """Round end of one client under round-complete delta gossip, one pass (elementwise.hip):
     ``u = y - x; cum += u; wire[:n] = cum; [cv = (x - y) inv_l - scale d; wire[n:] = cv];
-    y -= u; param_out = y``."""
+    y = x; param_out = x``."""
     if use_native(y):
         native().delta_round_end(y, x, cum, wire, param_out, d, cv, float(inv_l), float(scale))
         return

@@ -209,7 +209,7 @@ def delta_round_end_(y, x, cum, wire, param_out=None, d=None, cv=None, inv_l=0.0
             c = (-scale) * d + c
         cv.copy_(c)
         wire[n:].copy_(c)
-    y.add_(u, alpha=-1.0)
+    y.copy_(x)
     if param_out is not None and param_out.data_ptr() != y.data_ptr():
         param_out.copy_(y)
 

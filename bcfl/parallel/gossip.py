@@ -495,6 +495,7 @@ class MailboxGossip:
         self.applied_mid = 0
         self.pend: Optional[Dict[int, torch.Tensor]] = None   # see enable_self_delay
         self._fused: set = set()       # clients whose round end ran as one fused pass
+        self._start_live: set = set()  # ... whose start record still equals the live model
         self.fuse_round_end = True     # False: the separate passes (tests compare the two)
 
     def enable_self_delay(self) -> None:
@@ -532,7 +533,10 @@ class MailboxGossip:
         """Delta exchange: record hosted client c's round-start model (stream-ordered before its
         first optimizer step); its update u_c = y_c - x_c is formed at publish."""
         if self.exchange == "delta":
-            self.start[c].copy_(x)
+            if c in self._start_live:   # the fused round end left start == model, and every
+                self._start_live.discard(c)   # application since went to both: nothing to copy
+            else:
+                self.start[c].copy_(x)
             self._started.add(c)
 
     # ---- apply on arrival ---------------------------------------------------------------------
@@ -1000,6 +1004,9 @@ class MailboxGossip:
                                      buf if cv is not None else buf[: self.numel],
                                      (param_out or {}).get(c), d, cv, inv_l, sc)
                 self._fused.add(c)
+                # model == start again: applications until the next round start go to both
+                self._started.add(c)
+                self._start_live.add(c)
             else:
                 ops.cast_copy_(buf[: self.numel],
                                self.cum[c] if self.exchange == "delta" else self.states[c])
