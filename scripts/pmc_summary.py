@@ -13,8 +13,8 @@ for f in sorted(glob.glob(sys.argv[1] + "/p*/pmc_counter_collection.csv")):
         n = r["Kernel_Name"]
         if flt not in n:
             continue
-        m = re.search(r"::(\w+<\d+)", n)
-        k = m.group(1) + ">" if m else n[:50]
+        m = re.search(r"::(\w+<[^>]*>)", n)   # the full template argument list
+        k = m.group(1) if m else n[:50]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         agg[k]["dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, d in agg.items():
