@@ -874,11 +874,34 @@ class Federation:
         whatever the GPU count. Otherwise one model (client None = the model bound to
         ``self.flat``: the global model in server mode, the first hosted client in serverless)."""
         if self._sharded_eval():
+            if len(self.local_clients) > 1 and self._hosted_models_identical():
+                # every hosted client holds the same model: one model on the union of their
+                # strides scores exactly the same rows with exactly the same predictions, in
+                # fewer, larger forwards and with one snapshot instead of one per client
+                c0 = self.local_clients[0]
+                return [(c0, self._cached_batches(
+                    ("global", self._draw_key(r), "hosted"),
+                    lambda: ClientLoader(
+                        self.test_ds, np.sort(np.concatenate(
+                            [self._global_eval_rows(r, c) for c in self.local_clients])),
+                        max(self.cfg.global_eval_batch, 1),
+                        pad_multiple=self.pad_multiple).device_batches(self.device)))]
             return [(c, self.global_test_batches(r, c)) for c in self.local_clients]
         if self._average_eval():
             self._refresh_average()
             return [(-1, self.global_test_batches(r))]
         return [(None, self.global_test_batches(r))]
+
+    def _hosted_models_identical(self) -> bool:
+        """Round-complete delta gossip with every hosted client's round end fused: each model was
+        set back to its round-start record and every complete round was applied to all of them
+        with the same shared update, so they are bit-identical at the round end (the models of a
+        federation whose rounds are all complete are the same model)."""
+        g = self.gossip
+        return (isinstance(g, MailboxGossip) and g.exchange == "delta" and g.apply_mode == "complete"
+                and g._fused == set(self.local_clients) and not g.suppressed and not g.tamper
+                and self.filter is None and not self.cfg.inject_byzantine
+                and self.cfg.topology == "full" and self.cfg.mixing == "average")
 
     def _average_eval(self) -> bool:
         c = self.cfg

@@ -98,3 +98,28 @@ def test_fused_round_end_matches_separate_passes(tmp_path):
         torch.testing.assert_close(a.client_master[c], b.client_master[c], atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(a.gossip.cum[c], b.gossip.cum[c], atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(a.drift.cv[c], b.drift.cv[c], atol=1e-3, rtol=1e-4)
+
+
+def test_hosted_models_identical_and_scored_once(tmp_path, monkeypatch):
+    """Round-complete delta gossip with fused round ends leaves every hosted client holding the
+    same model at each round end (bit for bit), so the sharded global evaluation scores one model
+    on the union of the strides — with exactly the accuracies of scoring each client model on
+    its own stride."""
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    kw = dict(mode="serverless", model="tiny-bert", dataset="tiny", num_clients=4, num_rounds=3,
+              train_samples=48, test_samples=16, global_test_samples=64, batch_size=16, lr=1e-3,
+              partition="label_shards", reference_prints=False, save_every=0, device="cpu",
+              drift_correction="scaffold", ledger=False, gossip_transport="loopback",
+              loopback_lag_steps=[1, 2])
+    fed = Federation(FLConfig(out_dir=str(tmp_path / "a"), **kw), verbose=False)
+    seen = []
+    for r in range(3):
+        fed.run_round(r)
+        ms = [fed.client_master[c] for c in fed.local_clients]
+        seen.append(all(torch.equal(m, ms[0]) for m in ms[1:]) and fed._hosted_models_identical())
+    assert all(seen)
+    monkeypatch.setattr(Federation, "_hosted_models_identical", lambda self: False)
+    ref = Federation(FLConfig(out_dir=str(tmp_path / "b"), **kw), verbose=False)
+    ref.run()
+    assert fed.global_accuracies == ref.global_accuracies
