@@ -401,8 +401,12 @@ class Federation:
             # serverless 6 (8 clients: 6 lanes beat 8 in 4 / 4 interleaved reps, 0.548 vs 0.560
             # s/round; the box runs 4 hardware queues per process), server 8 (config 2, 4 steps per
             # client: 8 lanes beat 6, 0.338-0.345 vs 0.374-0.380; profiles/lanes_count_ab_r3.json)
+            # serverless with more than 8 hosted clients: 10 lanes (two waves of 10 at 20 clients,
+            # one at 10: 10 clients 0.400 vs 0.426 s/round with 6, 20 clients 0.734 vs 0.751,
+            # server 0.399 / 0.748; profiles/worker_grid_r5_lanes.json)
             big = sum(p.numel() for p in self.model.parameters()) > 1_000_000_000
-            n = min(2 if big else (8 if cfg.mode == "server" else 6), len(self.local_clients))
+            hosted = len(self.local_clients)
+            n = min(2 if big else (8 if cfg.mode == "server" else (6 if hosted <= 8 else 10)), hosted)
         n = max(1, min(n, len(self.local_clients)))
         lanes = []
         for i in range(n):
