@@ -1418,7 +1418,7 @@ class Federation:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
         need_prev = self.filter is not None or bool(cfg.inject_byzantine)
-        self._run_deferred()            # last round's host reads (its kernels have finished)
+        self._run_deferred(block=False)  # earlier rounds' host reads whose kernels have finished
         self._resolve_eval_local()      # last round's deferred local scores (long finished)
         lead_wait = self._bound_lead(r)
         self._round_now = r
@@ -1536,13 +1536,27 @@ class Federation:
 
     # ---- host reads deferred to the next round --------------------------------------------------
     def _defer(self, fn) -> None:
+        """Queue a host read of this round's device results. It runs once the work queued so far
+        has finished on the device (an event recorded now), so a read never stalls the host in
+        front of the next round's launches: at the next round start the round's tail is usually
+        still running, and the read waits one more round instead of idling the GPU."""
         if not hasattr(self, "_deferred"):
             self._deferred = []
-        self._deferred.append(fn)
+        ev = None
+        if self.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        self._deferred.append((fn, ev))
 
-    def _run_deferred(self) -> None:
-        fns, self._deferred = getattr(self, "_deferred", []), []
-        for fn in fns:
+    def _run_deferred(self, block: bool = True) -> None:
+        """Run the queued host reads in order; ``block=False`` stops at the first one whose
+        device work has not finished yet (it stays queued)."""
+        q = getattr(self, "_deferred", [])
+        while q:
+            fn, ev = q[0]
+            if not block and ev is not None and not ev.query():
+                break
+            q.pop(0)
             fn()
 
     def _local_metrics(self, local_eval: Dict[int, torch.Tensor]) -> list:
