@@ -324,6 +324,9 @@ class DriftCorrection:
               "ready": {int(c): bool(v) for c, v in self.ready.items()}}
         if self.exchange:
             st["cv"] = {int(c): t.detach().cpu().clone() for c, t in self.cv.items()}
+        if self.ring:   # round-tagged corrections (slot 0 is buf itself)
+            st["ring1"] = {int(c): r[1].detach().cpu().clone() for c, r in self.ring.items()}
+            st["ring_round"] = {int(c): list(v) for c, v in self.ring_round.items()}
         return st
 
     @torch.no_grad()
@@ -337,3 +340,8 @@ class DriftCorrection:
         if self.exchange and "cv" in st:
             for c, t in st["cv"].items():
                 self.cv[int(c)].copy_(t)
+        for c, t in st.get("ring1", {}).items():
+            c = int(c)
+            self.ring[c] = [self.buf[c], t.to(self.buf[c].device).clone()]
+            rr = st["ring_round"]
+            self.ring_round[c] = [int(x) for x in rr.get(c, rr.get(str(c), [-1, -1]))]

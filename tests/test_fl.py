@@ -476,3 +476,23 @@ def test_global_eval_every_k_rounds_and_the_last(tmp_out, mode):
     scored = [h["round"] for h in fed.history if h["global_acc"] is not None]
     assert scored == [1, 3, 4]
     assert len(fed.global_accuracies) == 3
+
+
+def test_uniform_gossip_mix_shared_sum_matches_per_client(tmp_path, monkeypatch):
+    """Average mixing on a complete graph (every entry of the mixing rows equal) with 5 hosted
+    clients: forming the sum of the published views once and giving each client w x_c +
+    w (S - view_c) matches the per-client n-term mixes up to fp32 summation order."""
+    from bcfl.parallel.gossip import GossipEngine
+    kw = dict(mode="serverless", num_clients=5, num_rounds=2, partition="iid_random",
+              save_every=0, ledger=False)
+    a = Federation(_cfg(str(tmp_path / "a"), **kw), verbose=False)
+    a.run()
+    D.set_runtime_for_tests(None)
+    monkeypatch.setattr(GossipEngine, "_uniform_rows", lambda self, W: False)
+    from bcfl.parallel import gossip as G
+    monkeypatch.setattr(G.MailboxGossip, "_uniform_rows", lambda self, W: False)
+    b = Federation(_cfg(str(tmp_path / "b"), **kw), verbose=False)
+    b.run()
+    assert getattr(a.gossip, "_mix_sum", None) is not None and getattr(b.gossip, "_mix_sum", None) is None
+    for c in a.local_clients:
+        torch.testing.assert_close(a.client_master[c], b.client_master[c], atol=1e-4, rtol=1e-4)
