@@ -1,12 +1,14 @@
 """Which eager torch ops (and D2D copies) run in a bench round: torch.profiler over one round of
 the bench federation, aggregated by op name + input shapes (host-side attribution of the
 'torch eager kernels' and copyBuffer rows of the rocprof summary)."""
+import os
 import sys
 
 import torch
 from torch.profiler import ProfilerActivity, profile
 
-import bcfl  # noqa: F401
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bcfl  # noqa: F401,E402
 from bcfl.config import get_preset
 from bcfl.fl import Federation
 
