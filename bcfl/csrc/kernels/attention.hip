@@ -313,7 +313,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t bits[2];
     float ls;
     {
-      ls = 0.f;
+      // exponent arguments and the row sum in packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two
+      // scores per VALU op), the exp itself per score
+      const f32x2_t sl2v = {sl2, sl2}, nmv = {-m, -m};
+      f32x2_t lsv = {0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         bits[t] = 0u;
@@ -321,9 +324,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int g4 = 0; g4 < 4; ++g4) {
           float pv[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            pv[e] = fexp2(fmaf(sacc[t][4 * g4 + e], sl2, -m));
-            ls += pv[e];
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2_t s2 = {sacc[t][4 * g4 + e], sacc[t][4 * g4 + e + 1]};
+            const f32x2_t a2 = __builtin_elementwise_fma(s2, sl2v, nmv);
+            pv[e] = fexp2(a2.x);
+            pv[e + 1] = fexp2(a2.y);
+            lsv += f32x2_t{pv[e], pv[e + 1]};
           }
           uint32_t w0 = pack2bf(pv[0], pv[1]), w1 = pack2bf(pv[2], pv[3]);
           if constexpr (DROP != 0) {
@@ -341,6 +347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           pw[2 * t + (g4 >> 1)][2 * (g4 & 1) + 1] = w1;
         }
       }
+      ls = lsv.x + lsv.y;
     }
     l += ls;
     if constexpr (DROP != 0) {  // publish this (query, 2 key blocks)'s decisions: half hh writes block hh
@@ -512,6 +519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int u = 0; u < HD / 32; ++u) dq[u] = zero16();
   const float sl2 = p.scale * LOG2E;
+  const f32x2_t sl2v = {sl2, sl2}, nlv = {-lse2, -lse2}, ndv = {-dlt, -dlt};
 
   TileOffsets<HD> to;
   to.init(lane);
@@ -577,16 +585,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
-        float ds[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int rg = reg + e;
-          const float pv = fexp2(fmaf(sacc[rg], sl2, -lse2));
-          float dp = pacc[rg];
-          if constexpr (DROP != 0) dp = keep_and(dp, wk, 8 * (rg & 3) + (rg >> 2));  // key 8 (rg >> 2) + 4 hh + (rg & 3)
-          ds[e] = pv * (dp - dlt);
+        // score pairs in packed fp32 (v_pk_fma / v_pk_add / v_pk_mul), the exp per score
+        const f32x2_t a2 = __builtin_elementwise_fma(f32x2_t{sacc[reg], sacc[reg + 1]}, sl2v, nlv);
+        f32x2_t dp = {pacc[reg], pacc[reg + 1]};
+        if constexpr (DROP != 0) {  // key 8 (rg >> 2) + 4 hh + (rg & 3)
+          dp.x = keep_and(dp.x, wk, 8 * (reg & 3) + (reg >> 2));
+          dp.y = keep_and(dp.y, wk, 8 * ((reg + 1) & 3) + ((reg + 1) >> 2));
         }
-        dsw[2 * t + (reg >> 3)][(reg & 7) >> 1] = pack2bf(ds[0], ds[1]);
+        const f32x2_t ds = f32x2_t{fexp2(a2.x), fexp2(a2.y)} * (dp + ndv);
+        dsw[2 * t + (reg >> 3)][(reg & 7) >> 1] = pack2bf(ds.x, ds.y);
       }
     };
     half(std::integral_constant<int, 0>{});

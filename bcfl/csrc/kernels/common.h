@@ -14,6 +14,7 @@ typedef uint16_t bf16_t;  // raw bf16 bits
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA A/B fragment (4 VGPRs)
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;     // packed-fp32 VALU pair
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;

@@ -187,20 +187,23 @@ def test_mailbox_failure_on_one_rank_falls_back_to_rccl_everywhere(tmp_path, how
 def _learn_worker(rank, world, out, kw):
     from bcfl.config import get_preset
     from bcfl.fl import Federation
-    torch.set_num_threads(2)
+    kw = dict(kw)
+    torch.set_num_threads(kw.pop("threads", 2))
     base = dict(model="tiny-bert", num_clients=4, num_rounds=16, mode="serverless", lr=2e-3,
                 lr_warmup_steps=8, max_seq_len=64, train_samples=256, global_test_samples=200,
                 eval_local=False, save_every=0, ledger=False, device="cpu",
                 reference_prints=False, out_dir=out, backend="gloo", gossip_transport="mailbox")
     base.update(kw)
     fed = Federation(get_preset("baseline3_learnable", **base), verbose=False)
+    t0 = time.perf_counter()
     fed.run()
     h = fed.history
     return {"fa": fed.federation_accuracy(), "same_round": fed.same_round_mix,
             "exchange": fed.drift.exchange, "delta": fed.gossip.exchange == "delta",
             "acc": torch.tensor([x["global_acc"] for x in h]),
             "stale_max": torch.tensor(max(float(x.get("stale_max") or 0.0) for x in h)),
-            "wait": torch.tensor(sum(float(x.get("wait_s") or 0.0) for x in h))}
+            "wait": torch.tensor(sum(float(x.get("wait_s") or 0.0) for x in h)),
+            "elapsed": torch.tensor(time.perf_counter() - t0)}
 
 
 def _check_async_learning(res):
@@ -239,9 +242,11 @@ def test_mailbox_async_two_ranks_slow_peer_default_protocol(tmp_path):
 @pytest.mark.slow
 def test_mailbox_async_four_ranks_learn_label_shards(tmp_path):
     """Same with one client per rank (every neighbour remote: every mix is stale). Both tests run
-    UNBOUNDED (gossip_max_lead = 0: no rank ever waits); the default bound is pinned below."""
+    UNBOUNDED (gossip_max_lead = 0: no rank ever waits); the default bound is pinned below. One
+    thread per rank: the ranks' relative pace (which nothing bounds here) then does not depend on
+    what else shares the 8 cores."""
     res = run_world(_learn_worker, 4, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"num_rounds": 20, "liveness_timeout": 6, "gossip_max_lead": 0})
+                    {"num_rounds": 20, "liveness_timeout": 6, "gossip_max_lead": 0, "threads": 1})
     _check_async_learning(res)
 
 
@@ -258,7 +263,9 @@ def test_mailbox_async_eight_ranks_default_protocol_learn_label_shards(tmp_path)
         assert not r["same_round"] and r["exchange"] and r["delta"]
         assert float(r["acc"][-3:].max()) >= 0.9, r["acc"].tolist()
         assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
-        assert float(r["wait"]) < 30.0   # the bound holds fast ranks back a little, never stalls
+        # the bound holds fast ranks back a little, never stalls (relative: the suite may share
+        # the 8 cores with other tests)
+        assert float(r["wait"]) < 0.5 * float(r["elapsed"]), (float(r["wait"]), float(r["elapsed"]))
 
 
 def test_mailbox_self_delay_runs_and_resumes_state(tmp_path):
