@@ -199,6 +199,12 @@ class FLConfig:
                                           # result lands in history[r] one round later (drain()
                                           # / finish() resolve the last one). None = auto: on for
                                           # collective-free GPU runs of models < 1e9 parameters
+    prefetch_batches: Optional[bool] = None  # GPU runs: pack (and pin) round r+1's training
+                                        # batches on a host thread while round r trains (the
+                                        # round start then only issues the H2D copy). None = auto:
+                                        # on with one client lane (the one-client-per-GPU layout:
+                                        # 1-client round 0.0937 -> 0.0903-0.0930 s), off with
+                                        # concurrent lanes (no gain, profiles/prefetch_ab_r5.json)
     metrics_jsonl: bool = True
     reference_prints: bool = True
     log_provenance: bool = True         # per-round sampled train/test indices (reference C18)

@@ -230,27 +230,42 @@ class ClientLoader:
         order = self._order(epoch)
         return [self._pack(order[i:i + self.batch_size]) for i in range(0, len(order), self.batch_size)]
 
-    def device_batches(self, device, epoch: Optional[int] = None) -> List[PackedBatch]:
-        """All batches of one epoch, staged with ONE pinned-buffer H2D copy."""
+    @staticmethod
+    def _parts(b: PackedBatch):
+        return [t for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.sort_ids,
+                            b.sort_pos, b.attn_sched) if t is not None]
+
+    def stage(self, epoch: Optional[int] = None, pin: bool = True):
+        """Host half of :meth:`device_batches`: the epoch's packed batches and ONE (pinned)
+        int32 buffer holding all of their index tensors. Pure host work (no device call), so it
+        can run on a prefetch thread while the previous round trains."""
         hb = self.host_batches(epoch)
         self.epoch += 1
-        dev = torch.device(device)
-        if dev.type != "cuda":
-            return hb
+        if not pin:
+            return hb, None
         flat = [x for b in hb for x in (b if isinstance(b, MicroBatches) else [b])]
-
-        def parts(b: PackedBatch):
-            return [t for t in (b.input_ids, b.position_ids, b.cu_seqlens, b.labels, b.sort_ids,
-                                b.sort_pos, b.attn_sched) if t is not None]
-
-        total = int(sum(t.numel() for b in flat for t in parts(b)))
+        total = int(sum(t.numel() for b in flat for t in self._parts(b)))
         host = torch.empty(total, dtype=torch.int32, pin_memory=True)
         off = 0
         for b in flat:
-            for t in parts(b):
+            for t in self._parts(b):
                 n = t.numel()
                 host[off:off + n].copy_(t.reshape(-1))
                 off += n
+        return hb, host
+
+    def device_batches(self, device, epoch: Optional[int] = None) -> List[PackedBatch]:
+        """All batches of one epoch, staged with ONE pinned-buffer H2D copy."""
+        dev = torch.device(device)
+        return self.upload(self.stage(epoch, pin=dev.type == "cuda"), dev)
+
+    def upload(self, staged, device) -> List[PackedBatch]:
+        """Device half: one H2D copy of the staged buffer on the current stream, then views."""
+        hb, host = staged
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            return hb
+        parts = self._parts
         devbuf = host.to(dev, non_blocking=True)
         off = 0
 

@@ -751,13 +751,18 @@ class Federation:
 
     def partitions(self, r: int):
         key = r if self.cfg.resample_each_round else 0
-        if key not in self._parts:
+        parts = self._parts.get(key)
+        if parts is None:
             c = self.cfg
-            self._parts = {key: partition_clients(c.partition, self.spec, self.train_ds.labels,
-                                                  self.test_ds.labels, c.num_clients,
-                                                  c.train_samples, c.test_samples, c.seed, key,
-                                                  c.dirichlet_alpha)}
-        return self._parts[key]
+            parts = partition_clients(c.partition, self.spec, self.train_ds.labels,
+                                      self.test_ds.labels, c.num_clients, c.train_samples,
+                                      c.test_samples, c.seed, key, c.dirichlet_alpha)
+            # keep the newest two draws: the batch prefetcher packs round r + 1 while round r
+            # still reads its own (a new dict, so a concurrent reader never sees a half update)
+            keep = {k: v for k, v in self._parts.items() if k == key - 1}
+            keep[key] = parts
+            self._parts = keep
+        return parts
 
     @property
     def steps_per_round(self) -> int:
@@ -806,12 +811,42 @@ class Federation:
         # GPU: bucket T to a multiple of 256 (stable GEMM shapes); CPU: exact shapes
         return 256 if self.is_cuda else 0
 
-    def train_batches(self, c: int, r: int, epoch: int):
+    def _train_loader(self, c: int, r: int) -> ClientLoader:
         sp = self.partitions(r)[c]
-        ld = ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
-                          seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple,
-                          split=self.micro_split, presort=self.is_cuda)
-        return ld.device_batches(self.device, epoch=r * self.cfg.local_epochs + epoch)
+        return ClientLoader(self.train_ds, sp.train, self.cfg.batch_size, shuffle=True,
+                            seed=_cseed(self.cfg.seed, c), pad_multiple=self.pad_multiple,
+                            split=self.micro_split, presort=self.is_cuda)
+
+    def _stage_train(self, c: int, r: int, epoch: int):
+        ld = self._train_loader(c, r)
+        return ld, ld.stage(r * self.cfg.local_epochs + epoch, pin=self.is_cuda)
+
+    def train_batches(self, c: int, r: int, epoch: int):
+        fut = getattr(self, "_prefetched", {}).pop((c, r, epoch), None)
+        ld, staged = fut.result() if fut is not None else self._stage_train(c, r, epoch)
+        return ld.upload(staged, self.device)
+
+    def _prefetch_train(self, r: int) -> None:
+        """Pack round r's training batches for every hosted client on a host thread (GPU runs).
+        Called at the start of round r - 1: the packing (numpy + one pinned buffer per client and
+        epoch) overlaps that round's training instead of delaying round r's first launches — with
+        one client per GPU the device otherwise idles for the packing at every round start. The
+        batches are a pure function of (client, round, epoch), so prefetched and inline batches are
+        identical."""
+        cfg = self.cfg
+        on = cfg.prefetch_batches if cfg.prefetch_batches is not None else len(self.lanes) <= 1
+        if not (self.is_cuda and on) or r >= cfg.num_rounds:
+            return
+        if not hasattr(self, "_prefetched"):
+            import concurrent.futures as cf
+            self._prefetched: Dict[tuple, object] = {}
+            self._prefetch_pool = cf.ThreadPoolExecutor(1, thread_name_prefix="bcfl-prefetch")
+        for k in [k for k in self._prefetched if k[1] < r - 1]:
+            self._prefetched.pop(k)   # rounds that never trained these clients (resume, sampling)
+        for c in self.local_clients:
+            for e in range(cfg.local_epochs):
+                if (c, r, e) not in self._prefetched:
+                    self._prefetched[(c, r, e)] = self._prefetch_pool.submit(self._stage_train, c, r, e)
 
     def _cached_batches(self, key, build):
         """Evaluation batches are a pure function of the (per-round when resampling) draw: build
@@ -1702,6 +1737,7 @@ class Federation:
         self._log_provenance(r)
         self.timer.begin_round()
         t0 = time.perf_counter()
+        self._prefetch_train(r + 1)   # packed on the host thread while round r trains
         res = self.server_round(r) if self.cfg.mode == "server" else self.serverless_round(r)
         ge: Optional[EvalResult] = res.get("global")
         gacc = ge.accuracy if ge is not None else None
@@ -1913,6 +1949,9 @@ class Federation:
         """Drain communication and I/O, verify the ledger (collective-free runs: cross-rank audit,
         a collective — pass ``audit=False`` when some rank has exited)."""
         self.drain()
+        if hasattr(self, "_prefetch_pool"):
+            self._prefetch_pool.shutdown(wait=True, cancel_futures=True)
+            self._prefetched.clear()
         if self.ckpt is not None:
             self.ckpt.close()
             if self.rt.is_main and self.cfg.compat_save_path and self.ckpt.last_dir:

@@ -14,16 +14,17 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _run(tmp, lanes, overlap):
+def _run(tmp, lanes, overlap, **kw):
     from bcfl.config import FLConfig
     from bcfl.fl import Federation
     from bcfl.parallel import dist as D
     D.set_runtime_for_tests(None)
+    kw.setdefault("num_rounds", 2)
     cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=4,
-                   num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                   train_samples=64, test_samples=32, global_test_samples=64,
                    out_dir=tmp, reference_prints=False, client_lanes=lanes, overlap_wgrad=overlap,
                    async_gossip=False, gossip_transport="rccl", ledger=True, save_every=0,
-                   dropout=0.1, drift_correction="scaffold")
+                   dropout=0.1, drift_correction="scaffold", **kw)
     fed = Federation(cfg, verbose=False)
     assert len(fed.lanes) == lanes
     h = fed.run()
@@ -49,6 +50,15 @@ def test_gpu_lanes_match_sequential(tmp_path, lanes, overlap):
     assert torch.equal(a[0], b[0]), f"lane run differs from one lane by {d:.3e}"
     assert a[1] == b[1]
     assert a[2] == b[2]
+
+
+def test_gpu_prefetched_batches_match_inline(tmp_path):
+    """Round r + 1's training batches packed on the host prefetch thread (pinned staging while
+    round r trains) are the inline batches: bit-identical masters, losses and ledger roots."""
+    a = _run(str(tmp_path / "inline"), 1, True, prefetch_batches=False, num_rounds=3)
+    b = _run(str(tmp_path / "pref"), 1, True, prefetch_batches=None, num_rounds=3)  # auto: on
+    assert torch.isfinite(a[0]).all()
+    assert torch.equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2]
 
 
 def test_gpu_lanes_close_to_sequential(tmp_path):
