@@ -32,8 +32,9 @@
 //
 // Dropout keep bits: the forward evaluates the counter hash (bcfl/ops/rng.py layout, one hash per
 // 4 scores) and also WRITES the decisions as a bitmask (1 bit per score, ~6 MB per BERT layer);
-// the dq and dkdv kernels read those bits back — 2 VALU ops per score (bit-field extract to a
-// 0 / -1 mask + AND) instead of re-hashing in each of them.
+// the dq and dkdv kernels read those bits back instead of re-hashing in each of them — dkdv with
+// 2 VALU ops per score (bit-field extract to a 0 / -1 mask + AND), dq with 1.5 (a byte-spread
+// word, v_cvt_f32_ubyte to 0.f / 1.f, the multiply folded into a packed fma).
 #include <math.h>
 
 #include <cstdio>
@@ -105,6 +106,18 @@ __device__ __forceinline__ float xor32_sum(float x) {
 __device__ __forceinline__ uint32_t xor32_get(uint32_t x, int hh) {
   const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
   return hh ? r[0] : r[1];
+}
+
+// byte B of x as a float (v_cvt_f32_ubyte{B}: one full-rate op; the compiler's own lowering of
+// (float)((x >> 8B) & 0xff) re-derives the bits with extra shifts when x is a masked word)
+template <int B>
+__device__ __forceinline__ float cvt_ubyte(uint32_t x) {
+  float r;
+  if constexpr (B == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(x));
+  if constexpr (B == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(x));
+  if constexpr (B == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(x));
+  if constexpr (B == 3) asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
 // bit of key j (0..31 inside its 32-key block) in a keep word (kernels.h)
@@ -584,16 +597,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
       }
 #pragma unroll
-      for (int reg = 0; reg < 16; reg += 2) {
-        // score pairs in packed fp32 (v_pk_fma / v_pk_add / v_pk_mul), the exp per score
-        const f32x2_t a2 = __builtin_elementwise_fma(f32x2_t{sacc[reg], sacc[reg + 1]}, sl2v, nlv);
-        f32x2_t dp = {pacc[reg], pacc[reg + 1]};
-        if constexpr (DROP != 0) {  // key 8 (rg >> 2) + 4 hh + (rg & 3)
-          dp.x = keep_and(dp.x, wk, 8 * (reg & 3) + (reg >> 2));
-          dp.y = keep_and(dp.y, wk, 8 * ((reg + 1) & 3) + ((reg + 1) >> 2));
+      for (int g = 0; g < 4; ++g) {
+        // accumulator rows 4g + e hold keep bit 8e + g of the word (key 8 g + 4 hh + e): one
+        // shift + and leaves byte e = that bit, v_cvt_f32_ubyte{e} turns it into 0.f / 1.f, and
+        // the multiply rides in the packed fma dp * keep - delta (1.5 VALU ops per score for
+        // dropout instead of 2)
+        uint32_t kb = 0x01010101u;
+        if constexpr (DROP != 0) kb = (wk >> g) & 0x01010101u;
+        const f32x2_t k01 = {cvt_ubyte<0>(kb), cvt_ubyte<1>(kb)};
+        const f32x2_t k23 = {cvt_ubyte<2>(kb), cvt_ubyte<3>(kb)};
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int reg = 4 * g + e;
+          // score pairs in packed fp32 (v_pk_fma / v_pk_mul), the exp per score
+          const f32x2_t a2 = __builtin_elementwise_fma(f32x2_t{sacc[reg], sacc[reg + 1]}, sl2v, nlv);
+          const f32x2_t dp = {pacc[reg], pacc[reg + 1]};
+          const f32x2_t kd = DROP != 0 ? __builtin_elementwise_fma(dp, e ? k23 : k01, ndv) : dp + ndv;
+          const f32x2_t ds = f32x2_t{fexp2(a2.x), fexp2(a2.y)} * kd;
+          dsw[2 * t + (reg >> 3)][(reg & 7) >> 1] = pack2bf(ds.x, ds.y);
         }
-        const f32x2_t ds = f32x2_t{fexp2(a2.x), fexp2(a2.y)} * (dp + ndv);
-        dsw[2 * t + (reg >> 3)][(reg & 7) >> 1] = pack2bf(ds.x, ds.y);
       }
     };
     half(std::integral_constant<int, 0>{});
