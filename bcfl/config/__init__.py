@@ -68,6 +68,9 @@ class FLConfig:
     #                                     AdamW learns (0.904 / 0.959) and kept moments do not
     #                                     (0.669 / 0.50); the CPU tiny-bert 8-rank case at lr 5e-4
     #                                     is the opposite (profiles/multirank_async_r4.json)
+    update_clip_ratio: float = 0.0      # per-round trust region: a client's round update
+                                        # x_end - x_start is scaled down to at most this fraction
+                                        # of ||x_start|| before it is averaged / published (0 = off)
     max_grad_norm: float = 0.0          # global-norm gradient clipping per local step (0 = off:
                                         # the reference's plain loop); fused into the AdamW pass
     drift_correction: str = "none"      # none | scaffold | auto (control variates in update

@@ -602,6 +602,8 @@ class Federation:
             if c in cfg.inject_slow:
                 time.sleep(cfg.inject_slow[c] / 1000.0)
             with self._on(lane):
+                if prev is not None:
+                    self._clip_update(self._update_ref(c, prev), lane.flat)
                 self.drift.after_train(c, lane.flat.master, self.lr_sum(r, st["batches"]))
                 self._phase[c] = "trained"
                 self.drift.detach(lane.opt)
@@ -675,6 +677,7 @@ class Federation:
             if c in cfg.inject_slow:
                 time.sleep(cfg.inject_slow[c] / 1000.0)
             with self._on(lane):
+                self._clip_update(G, lane.flat)
                 self.drift.after_train(c, lane.flat.master, self.lr_sum(r, st["batches"]))
                 self.drift.detach(lane.opt)
                 self._inject_byzantine(c, G, lane.flat)
@@ -1068,6 +1071,22 @@ class Federation:
         flat.sync_param_from_master()
 
     @torch.no_grad()
+    def _clip_update(self, ref: torch.Tensor, flat: Optional[FlatParams] = None) -> None:
+        """Per-round trust region (``update_clip_ratio``): scale the round's update x - ref down
+        to at most ratio * ||ref|| (device-side scalar, no host read). Early in training from
+        random init a client's Adam-normalised round update can be large enough to throw a model
+        that has just found the signal back onto the plateau."""
+        rho = float(self.cfg.update_clip_ratio)
+        if rho <= 0:
+            return
+        flat = flat or self.flat
+        m = flat.master
+        m.sub_(ref)
+        scale = torch.clamp(rho * ref.norm() / (m.norm() + 1e-12), max=1.0)
+        m.mul_(scale).add_(ref)
+        flat.sync_param_from_master()
+
+    @torch.no_grad()
     def _update_stats(self, ref: torch.Tensor, flat: Optional[FlatParams] = None):
         d = (flat or self.flat).master - ref
         return ops.block_sketch(d, self.cfg.sketch_dim).float(), d.norm().float()
@@ -1276,6 +1295,7 @@ class Federation:
             if self.verbose and cfg.reference_prints:
                 print("Training Started...", flush=True)
             st = self._train_client(c, r)
+            self._clip_update(G)
             self.drift.after_train(c, self.flat.master, self.lr_sum(r, st["batches"]))
             self.drift.detach(self.opt)
             self._inject_byzantine(c, G)
@@ -1452,7 +1472,8 @@ class Federation:
         if cfg.compat_chain:
             return self._chain_round(r)
         recs, sk, nr, losses, local_eval = [], {}, {}, {}, {}
-        need_prev = self.filter is not None or bool(cfg.inject_byzantine)
+        need_prev = (self.filter is not None or bool(cfg.inject_byzantine)
+                     or cfg.update_clip_ratio > 0)
         self._run_deferred(block=False)  # earlier rounds' host reads whose kernels have finished
         self._resolve_eval_local()      # last round's deferred local scores (long finished)
         lead_wait = self._bound_lead(r)
@@ -1472,6 +1493,8 @@ class Federation:
             self._activate(c)
             prev = self.flat.master.detach().clone() if need_prev else None
             st = self._train_client(c, r)
+            if prev is not None:
+                self._clip_update(self._update_ref(c, prev))
             self.drift.after_train(c, self.flat.master, self.lr_sum(r, st["batches"]))
             self._phase[c] = "trained"
             self.drift.detach(self.opt)

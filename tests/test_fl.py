@@ -53,6 +53,26 @@ def test_server_round_is_weighted_fedavg(tmp_out):
     torch.testing.assert_close(fed.global_master, expect, atol=1e-6, rtol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["server", "serverless"])
+def test_update_clip_ratio_bounds_the_round_update(tmp_out, mode):
+    """update_clip_ratio (per-round trust region): every client's round update is scaled to at
+    most ratio * ||x_start||. All clients start from the same model here, so the FedAvg step (server)
+    and a client's mixed model (serverless: a convex combination of clipped updates) obey the same
+    bound; off (0) the step is far larger."""
+    rho = 1e-4
+    steps = {}
+    for r_ in (0.0, rho):
+        cfg = _cfg(tmp_out, mode=mode, num_rounds=1, ledger=False, save_every=0,
+                   train_samples=40, update_clip_ratio=r_, async_gossip=False)
+        fed = Federation(cfg, verbose=False)
+        g0 = (fed.global_master if mode == "server" else fed.client_master[0]).clone()
+        fed.run_round(0)
+        g1 = fed.global_master if mode == "server" else fed.client_master[0]
+        steps[r_] = (float((g1 - g0).norm()), float(g0.norm()))
+    assert steps[0.0][0] > 2 * rho * steps[0.0][1]          # the bound binds here
+    assert steps[rho][0] <= rho * steps[rho][1] * (1 + 1e-3)
+
+
 def test_serverless_compat_chain(tmp_out):
     cfg = _cfg(tmp_out, mode="serverless", compat_chain=True, ledger=False, save_every=0)
     fed = Federation(cfg, verbose=False)
