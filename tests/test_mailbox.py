@@ -210,12 +210,13 @@ def _learn_worker(rank, world, out, kw):
 
 
 def _check_async_learning(res, last=3, final=None):
+    # accuracies travel as float32 tensors (0.9 arrives as 0.89999998): thresholds carry 1e-6
     for r in res:
         assert not r["same_round"] and r["exchange"] and r["delta"]
         assert float(r["wait"]) == 0.0                    # nothing ever waited on a peer
-        assert float(r["acc"][-last:].max()) >= 0.9, r["acc"].tolist()
+        assert float(r["acc"][-last:].max()) >= 0.9 - 1e-6, r["acc"].tolist()
         if final is not None:
-            assert float(r["fa"]["accuracy"]) >= final, (r["fa"], r["acc"].tolist())
+            assert float(r["fa"]["accuracy"]) >= final - 1e-6, (r["fa"], r["acc"].tolist())
     assert max(float(r["stale_max"]) for r in res) >= 1.0   # the mixes really were stale
 
 
@@ -240,8 +241,8 @@ def test_mailbox_async_two_ranks_slow_peer_default_protocol(tmp_path):
                     {"inject_slow": {1: 200.0}, "num_rounds": 20})
     for r in res:
         assert not r["same_round"] and r["exchange"] and r["delta"]
-        assert float(r["acc"][-3:].max()) >= 0.9, r["acc"].tolist()
-        assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
+        assert float(r["acc"][-3:].max()) >= 0.9 - 1e-6, r["acc"].tolist()
+        assert float(r["fa"]["accuracy"]) >= 0.9 - 1e-6, r["fa"]
 
 
 @pytest.mark.slow
@@ -268,8 +269,8 @@ def test_mailbox_async_eight_ranks_default_protocol_learn_label_shards(tmp_path)
                     {"num_clients": 8, "num_rounds": 30})
     for r in res:
         assert not r["same_round"] and r["exchange"] and r["delta"]
-        assert float(r["acc"][-3:].max()) >= 0.9, r["acc"].tolist()
-        assert float(r["fa"]["accuracy"]) >= 0.9, r["fa"]
+        assert float(r["acc"][-3:].max()) >= 0.9 - 1e-6, r["acc"].tolist()
+        assert float(r["fa"]["accuracy"]) >= 0.9 - 1e-6, r["fa"]
         # the bound holds fast ranks back a little, never stalls (relative: the suite may share
         # the 8 cores with other tests)
         assert float(r["wait"]) < 0.5 * float(r["elapsed"]), (float(r["wait"]), float(r["elapsed"]))
