@@ -205,9 +205,9 @@ class FLConfig:
     prefetch_batches: Optional[bool] = None  # GPU runs: pack (and pin) round r+1's training
                                         # batches on a host thread while round r trains (the
                                         # round start then only issues the H2D copy). None = auto:
-                                        # on with one client lane (the one-client-per-GPU layout:
-                                        # 1-client round 0.0937 -> 0.0903-0.0930 s), off with
-                                        # concurrent lanes (no gain, profiles/prefetch_ab_r5.json)
+                                        # on with up to 4 client lanes (the 8-, 4- and 2-GPU layouts:
+                                        # 1 client 0.0937 -> 0.0903-0.0930 s, 2 clients 0.157 ->
+                                        # 0.147), off with 8 (no gain; profiles/prefetch_ab_r5.json)
     metrics_jsonl: bool = True
     reference_prints: bool = True
     log_provenance: bool = True         # per-round sampled train/test indices (reference C18)

@@ -837,7 +837,7 @@ class Federation:
         batches are a pure function of (client, round, epoch), so prefetched and inline batches are
         identical."""
         cfg = self.cfg
-        on = cfg.prefetch_batches if cfg.prefetch_batches is not None else len(self.lanes) <= 1
+        on = cfg.prefetch_batches if cfg.prefetch_batches is not None else len(self.lanes) <= 4
         if not (self.is_cuda and on) or r >= cfg.num_rounds:
             return
         if not hasattr(self, "_prefetched"):
