@@ -32,6 +32,7 @@ def run_sweep(cfg) -> List[dict]:
         hist = fed.run()
         out.append({"num_clients": int(n), "rounds": len(hist),
                     "global_accuracies": list(fed.global_accuracies),
+                    "global_accuracy_rounds": list(fed.global_accuracy_rounds),
                     "mean_round_s": sum(h["t_round"] for h in hist) / max(len(hist), 1)})
     return out
 

@@ -158,6 +158,16 @@ class FLConfig:
                                         # the mailboxes: each rank owns 1/world of the buffer, each
                                         # link carries 1/world of the model; dead ranks left out)
     server_timeout_s: float = 120.0     # mailbox server: how long a round waits for a rank's post
+    server_holdout: int = 0             # server: rows of a validation slice (train-split rows no
+    #                                     client trains on) that score every new global model; a
+    #                                     model more than server_holdout_tol below the best so far
+    #                                     is not adopted (the previous global model is kept for the
+    #                                     next round) — 0 = off (Flower FedAvg adopts every result)
+    server_holdout_tol: float = 0.05
+    server_holdout_patience: int = 0    # > 0: after this many rejections in a row the next result
+    #                                     is adopted anyway; 0: pure model selection (a rejected
+    #                                     round is undone — global model and the clients' kept
+    #                                     optimizer states — and the next round retries from it)
     overlap_optimizer: bool = False     # one-lane GPU ranks: per-layer AdamW on a side stream
     #                                     launched from the gradient hooks mid-backward (bitwise;
     #                                     measured slower on BERT-base, so off by default)
@@ -386,6 +396,9 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # the 8-client federation learns whatever the post lag (0.97-0.996 after 25 rounds, lags 0-8
     # local steps); at lr 2e-5 / full correction the same protocol is slower (0.93) and with
     # mid-round application of partial rounds (round 4) it does not learn under jitter (0.51).
+    # Constant rate after the warm-up: on MI355X cosine decay over the bench's 25 rounds ends
+    # lower (0.959 vs 0.992 final accuracy, same tree, profiles/bench_r6_lr_schedule_ab.json) —
+    # the decayed late rounds no longer finish the label-shard consensus.
     "baseline3_learnable": dict(mode="serverless", model="bert-base", dataset="imdb", num_labels=2,
                                 num_clients=8, num_rounds=20, partition="label_shards",
                                 train_samples=240, test_samples=60, async_gossip=True, lr=4e-5,
@@ -429,8 +442,15 @@ _LEARNABLE = dict(lr=4e-5, lr_warmup_steps=24, keep_optimizer_state=False, synth
 # and cosine decay, moments kept across rounds, learns in both modes (worker grid at 5 / 10 / 20
 # clients: serverless 0.999 / 0.997 / 0.999, server 0.988 / 0.892 / 0.987;
 # profiles/worker_grid_r4_iid_protocol.json; the sweep behind it: profiles/iid_sweep_r4.json)
+# Server mode adds hold-out selection (round 6): the server scores every new global model on 256
+# train rows no client uses and keeps the previous global model (and the clients' kept AdamW
+# moments) when the new one falls more than 0.05 below the best — the post-convergence dips of the
+# server curves (config 2: 0.99 -> 0.73 / 0.64 at rounds 9-11,
+# profiles/bench_config2_server_fedavg_r5.json) come from aggregated updates that memorise the
+# clients' shared 100-row draw. A forced adoption after 3 rejections (first try) re-admitted them
+# (server, 20 clients: 0.986 -> 0.509, profiles/server_holdout_r6.json).
 IID_PROTOCOL = dict(lr=1e-4, adam_betas=(0.9, 0.98), max_grad_norm=1.0, lr_warmup_steps=24,
-                    lr_schedule="cosine", keep_optimizer_state=True)
+                    lr_schedule="cosine", keep_optimizer_state=True, server_holdout=256)
 _LEARNABLE_IID = {**_LEARNABLE, **IID_PROTOCOL}
 PRESETS["baseline2_learnable"] = {**PRESETS["baseline2_bert_server_iid"], **_LEARNABLE_IID}
 PRESETS["baseline4_learnable"] = {**PRESETS["baseline4_biobert_serverless_noniid_trust"], **_LEARNABLE}

@@ -624,6 +624,19 @@ Tensor block_sketch(Tensor x, int64_t dim, int64_t ka, int64_t kb) {
   return out;
 }
 
+Tensor update_stats(Tensor a, Tensor b, int64_t dim, int64_t ka, int64_t kb) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.numel() == b.numel() && a.scalar_type() == b.scalar_type(),
+              "update_stats: operands must match in size and dtype");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "update_stats: contiguous operands");
+  auto out = torch::empty({2 * dim}, a.options().dtype(torch::kFloat));
+  check_rc(bcfl::launch_update_stats(a.data_ptr(), b.data_ptr(), dt_of(a), a.numel(), (int)dim,
+                                     (uint32_t)ka, (uint32_t)kb, out.data_ptr<float>(), stream()),
+           "update_stats");
+  return out;
+}
+
 Tensor sha256_leaves(Tensor buf, int64_t leaf_bytes) {
   check_cuda(buf, "buf");
   const int64_t nbytes = buf.numel() * buf.element_size();
@@ -1140,6 +1153,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("delta_round_end", &delta_round_end);
   m.def("delta_encode", &delta_encode);
   m.def("block_sketch", &block_sketch);
+  m.def("update_stats", &update_stats);
   m.def("sha256_leaves", &sha256_leaves);
   m.def("sha256_merkle", &sha256_merkle);
   bcfl_comm::register_mailbox(m);

@@ -544,6 +544,44 @@ __global__ __launch_bounds__(EW_THREADS) void block_sketch_kernel(const TX* __re
   }
 }
 
+// update statistics of the anomaly filter, measured by the RECEIVER on what it is about to apply:
+// the signed block sketch of d = a - b (a = a source's newest cumulative update, b = the one
+// already applied) in out[0, dim) and the per-block sum of d^2 in out[dim, 2 dim) — one read of
+// each operand, no materialised difference
+template <typename T>
+__global__ __launch_bounds__(EW_THREADS) void update_stats_kernel(const T* __restrict__ a,
+                                                                  const T* __restrict__ b,
+                                                                  int64_t n, int64_t blk,
+                                                                  uint32_t ka, uint32_t kb,
+                                                                  float* __restrict__ out) {
+  __shared__ float red[2][EW_THREADS / WAVE];
+  const int64_t lo = (int64_t)blockIdx.x * blk;
+  const int64_t hi = lo + blk < n ? lo + blk : n;
+  float sk = 0.f, sq = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += EW_THREADS) {
+    const float d = ld<T>(a, i) - ld<T>(b, i);
+    const uint32_t h = hash32((uint32_t)i, ka, kb);
+    sk += (h & 1u) ? d : -d;
+    sq += d * d;
+  }
+  sk = wave_sum(sk);
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = sk;
+    red[1][threadIdx.x >> 6] = sq;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f, q = 0.f;
+    for (int w = 0; w < EW_THREADS / WAVE; ++w) {
+      t += red[0][w];
+      q += red[1][w];
+    }
+    out[blockIdx.x] = t;
+    out[gridDim.x + blockIdx.x] = q;
+  }
+}
+
 // dropout multiplier m[i] = keep(i) / (1 - p) or 0 (bcfl/ops/rng.py element layout): the pooled
 // [B, H] head dropout applies it with one multiply forward and one backward
 template <typename T>
@@ -848,6 +886,18 @@ int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka
     hipLaunchKernelGGL(block_sketch_kernel<bf16_t>, dim3(dim), dim3(EW_THREADS), 0, s, (const bf16_t*)x, n, blk, ka, kb, out);
   else
     hipLaunchKernelGGL(block_sketch_kernel<float>, dim3(dim), dim3(EW_THREADS), 0, s, (const float*)x, n, blk, ka, kb, out);
+  return 0;
+}
+
+int launch_update_stats(const void* a, const void* b, int dt, int64_t n, int dim, uint32_t ka,
+                        uint32_t kb, float* out, hipStream_t s) {
+  const int64_t blk = (n + dim - 1) / dim;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(update_stats_kernel<bf16_t>, dim3(dim), dim3(EW_THREADS), 0, s,
+                       (const bf16_t*)a, (const bf16_t*)b, n, blk, ka, kb, out);
+  else
+    hipLaunchKernelGGL(update_stats_kernel<float>, dim3(dim), dim3(EW_THREADS), 0, s,
+                       (const float*)a, (const float*)b, n, blk, ka, kb, out);
   return 0;
 }
 

@@ -33,10 +33,6 @@ int launch_emb_ln_fwd(const int* ids, const int* pos, const int* tt, const void*
                       const void* posw, const void* typew, const void* gamma, const void* beta,
                       void* out, void* z, float* mean, float* rstd, int T, int H, float eps,
                       uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
-int launch_emb_ln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
-                      const void* gamma, const int* ids, const int* pos, const int* tt,
-                      float* dword, float* dpos, float* dtype, float* partial, int nblk, int T,
-                      int H, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s);
 int launch_rmsnorm_fwd(const void* x, const void* w, void* out, float* rstd, int T, int H,
                        float eps, int dt, hipStream_t s);
 int launch_rmsnorm_bwd(const void* dout, const void* x, const void* w, const float* rstd, void* dx,
@@ -82,6 +78,8 @@ int64_t sumsq_mt_blocks(const int64_t* numels, int ntens);
 int launch_clip_coef_mt(const void* const* grads, const void* const* grads2, const int64_t* numels,
                         int ntens, int grad_dt, float* partial, float max_norm, float* out,
                         hipStream_t s);
+int launch_update_stats(const void* a, const void* b, int dt, int64_t n, int dim, uint32_t ka,
+                        uint32_t kb, float* out, hipStream_t s);
 int launch_block_sketch(const void* x, int x_dt, int64_t n, int dim, uint32_t ka, uint32_t kb,
                         float* out, hipStream_t s);
 

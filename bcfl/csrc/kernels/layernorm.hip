@@ -722,90 +722,6 @@ __global__ __launch_bounds__(LN_THREADS) void emb_ln_fwd_kernel(
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
-// partial k: 0 dgamma, 1 dbeta, 2 dtype-row-0 (when type ids are implicit zeros)
-template <typename TA, typename TP, int NCH>
-__global__ __launch_bounds__(LN_THREADS) void emb_ln_bwd_kernel(
-    const TA* __restrict__ dout, const TA* __restrict__ z, const float* __restrict__ mean_in,
-    const float* __restrict__ rstd_in, const TP* __restrict__ gamma, const int* __restrict__ ids,
-    const int* __restrict__ pos, const int* __restrict__ tt, float* __restrict__ dword,
-    float* __restrict__ dpos, float* __restrict__ dtype, float* __restrict__ partial, int T, int H,
-    uint32_t p8, uint32_t ka, uint32_t kb) {
-  __shared__ float red[LN_WAVES][3][NCH * 4 * WAVE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const float sc = p8 ? keep_scale(p8) : 1.f;
-  const bool type_sum = dtype != nullptr && tt == nullptr;
-  float dg[NCH][4], db[NCH][4], dt[NCH][4], gm[NCH][4];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int col = (lane + i * WAVE) * 4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dg[i][k] = db[i][k] = dt[i][k] = 0.f;
-    if (col < H) Vec4<TP>::load(gamma + col, gm[i]);
-  }
-  for (int row = blockIdx.x * LN_WAVES + wid; row < T; row += gridDim.x * LN_WAVES) {
-    const size_t base = (size_t)row * H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NCH][4], g[NCH][4];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int col = (lane + i * WAVE) * 4;
-      if (col < H) {
-        float d[4], zz[4];
-        Vec4<TA>::load(dout + base + col, d);
-        Vec4<TA>::load(z + base + col, zz);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (p8) d[k] = keep_elem((uint32_t)(base + col + k), p8, ka, kb) ? d[k] * sc : 0.f;
-          xh[i][k] = (zz[k] - mean) * rstd;
-          g[i][k] = d[k] * gm[i][k];
-          s1 += g[i][k];
-          s2 += g[i][k] * xh[i][k];
-          dg[i][k] += d[k] * xh[i][k];
-          db[i][k] += d[k];
-        }
-      }
-    }
-    s1 = wave_sum(s1) / H;
-    s2 = wave_sum(s2) / H;
-    const size_t wb = (size_t)ids[row] * H;
-    const size_t pb = dpos ? (size_t)pos[row] * H : 0;
-    const size_t tb = (dtype && tt) ? (size_t)tt[row] * H : 0;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int col = (lane + i * WAVE) * 4;
-      if (col < H) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float dz = rstd * (g[i][k] - s1 - xh[i][k] * s2);
-          atomicAdd(dword + wb + col + k, dz);
-          if (dpos) atomicAdd(dpos + pb + col + k, dz);
-          if (dtype && tt) atomicAdd(dtype + tb + col + k, dz);
-          if (type_sum) dt[i][k] += dz;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NCH; ++i)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int j = (i * WAVE + lane) * 4 + k;
-      red[wid][0][j] = dg[i][k];
-      red[wid][1][j] = db[i][k];
-      red[wid][2][j] = dt[i][k];
-    }
-  __syncthreads();
-  for (int j = threadIdx.x; j < H; j += LN_THREADS) {
-    for (int k = 0; k < 3; ++k) {
-      float a = 0.f;
-#pragma unroll
-      for (int w = 0; w < LN_WAVES; ++w) a += red[w][k][j];
-      partial[((size_t)blockIdx.x * 3 + k) * H + j] = a;
-    }
-  }
-}
-
 // ----------------------------------------- RMSNorm -------------------------------------------------
 // Wide-row forms (bf16, H % 512 == 0: Llama's 4096): one row per wave, 16-byte lanes (the 1 KiB
 // wave instruction), the row kept in registers as packed bf16 (4 VGPRs per 8 values) so NC8 = 8
@@ -1150,17 +1066,6 @@ int launch_emb_ln_fwd(const int* ids, const int* pos, const int* tt, const void*
   DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((emb_ln_fwd_kernel<TA, TP, NC>), grid,
       dim3(LN_THREADS), 0, s, ids, pos, tt, (const TP*)word, (const TP*)posw, (const TP*)typew,
       (const TP*)gamma, (const TP*)beta, (TA*)out, (TA*)z, mean, rstd, T, H, eps, p8, ka, kb)));
-  return 0;
-}
-
-int launch_emb_ln_bwd(const void* dout, const void* z, const float* mean, const float* rstd,
-                      const void* gamma, const int* ids, const int* pos, const int* tt,
-                      float* dword, float* dpos, float* dtype, float* partial, int nblk, int T,
-                      int H, uint32_t p8, uint32_t ka, uint32_t kb, int dt, hipStream_t s) {
-  if (H % 4) return -2;
-  DT_DISPATCH(dt, NCH_DISPATCH_SMALL(H, hipLaunchKernelGGL((emb_ln_bwd_kernel<TA, TP, NC>), dim3(nblk),
-      dim3(LN_THREADS), 0, s, (const TA*)dout, (const TA*)z, mean, rstd, (const TP*)gamma, ids,
-      pos, tt, dword, dpos, dtype, partial, T, H, p8, ka, kb)));
   return 0;
 }
 

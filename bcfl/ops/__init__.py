@@ -7,7 +7,7 @@ from .functional import (bias_dropout_add_layernorm, layernorm, bias_act, varlen
                          wgrad, set_wgrad_overlap, wgrad_overlap_enabled, join_wgrad, linear_act,
                          linear_after_act, gemm_supported, lora_linear, lora_swiglu_mlp,
                          xent_stats_, ResidualTap)
-from .flat import (adamw_, adamw_multi_, grad_clip_coef, gossip_mix_, weighted_accumulate_, block_sketch, scale_, axpby_,
+from .flat import (adamw_, adamw_multi_, grad_clip_coef, gossip_mix_, weighted_accumulate_, block_sketch, update_stats, scale_, axpby_,
                    delta_round_end_,
                    cast_copy_, merkle_root_sha256, merkle_root_deferred, root_bytes,
                    leaf_digests_sha256)
@@ -18,7 +18,7 @@ __all__ = [
     "embedding_layernorm", "rmsnorm", "rope", "swiglu", "cross_entropy", "linear", "dropout", "wgrad",
     "set_wgrad_overlap", "wgrad_overlap_enabled", "join_wgrad", "linear_act", "linear_after_act",
     "gemm_supported", "lora_linear", "lora_swiglu_mlp", "xent_stats_", "ResidualTap",
-    "adamw_", "adamw_multi_", "grad_clip_coef", "gossip_mix_", "weighted_accumulate_", "block_sketch", "scale_", "axpby_",
+    "adamw_", "adamw_multi_", "grad_clip_coef", "gossip_mix_", "weighted_accumulate_", "block_sketch", "update_stats", "scale_", "axpby_",
     "delta_round_end_",
     "cast_copy_", "merkle_root_sha256", "merkle_root_deferred", "root_bytes", "leaf_digests_sha256",
 ]

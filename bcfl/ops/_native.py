@@ -39,6 +39,9 @@ def native():
     m = _load()
     if m is None:
         raise RuntimeError("bcfl native extension unavailable on a GPU code path: " + str(_ERR))
+    from ..utils import streamcheck
+    if streamcheck.enabled():   # BCFL_DEBUG_STREAMS: every kernel call reported to the checker
+        return streamcheck.wrap_native(m)
     return m
 
 

@@ -149,6 +149,19 @@ def block_sketch(x: torch.Tensor, dim: int, seed: int = 0x5EED) -> torch.Tensor:
     return ref.block_sketch(x, dim, seed)
 
 
+def update_stats(a: torch.Tensor, b: torch.Tensor, dim: int, seed: int = 0x5EED):
+    """Anomaly-filter statistics of the update ``a - b`` without materialising it: its signed
+    block sketch (as :func:`block_sketch`) and its L2 norm, both device fp32 (one fused pass over
+    the two operands on GPU; no host sync)."""
+    if use_native(a):
+        from .rng import derive_keys
+        ka, kb = derive_keys(seed, 0)
+        out = native().update_stats(a.contiguous(), b.contiguous(), int(dim), int(ka), int(kb))
+        return out[:dim], out[dim:].sum().sqrt()
+    d = a.reshape(-1).float() - b.reshape(-1).float()
+    return ref.block_sketch(d, dim, seed), d.norm()
+
+
 # ------------------------------- SHA-256 Merkle ----------------------------------------------
 
 def _np_bytes(buf: torch.Tensor) -> np.ndarray:

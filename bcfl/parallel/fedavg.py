@@ -257,6 +257,7 @@ class MailboxReduceScatterFedAvg:
         self.bytes_posted = 0
         self.epoch = 0
         self.prev_live_mask = (1 << W) - 1
+        self.last_seen: Dict[int, int] = {p: 0 for p in self.peers}   # newest version seen
         self._done = None
 
     def _key(self, v: int, phase: int, who: int) -> int:
@@ -314,9 +315,24 @@ class MailboxReduceScatterFedAvg:
                 good[p] = sn
         return good
 
+    def _newest_peer_version(self) -> int:
+        """Newest aggregation epoch any peer has posted (reduce or gather inbox), 0 if none."""
+        best = 0
+        for tr in (self.rs, self.ag):
+            for h in tr.headers(self.peers).values():
+                nw = tr.newest(h)
+                if nw is not None:
+                    best = max(best, int(nw[1].version))
+        return best
+
     def reduce(self, r: int, partial: torch.Tensor, w_local: float) -> Tuple[torch.Tensor, Dict]:
         W, k, n = self.world, self.rank, self.numel
-        v = self.epoch + 1
+        # aggregation epoch = the posts' version, with MailboxFedAvg's catch-up rule: a rank that
+        # finds a peer already further (started late, or excluded as slow for several rounds)
+        # posts into the federation's current epoch instead of fetching versions its peers have
+        # long overwritten (it would otherwise wait out two timeouts every round and never rejoin)
+        v = max(self.epoch + 1, self._newest_peer_version())
+        skipped = v - self.epoch - 1
         self.epoch = v
         slot = v % 2
         b0 = self.rs.bytes_posted + self.ag.bytes_posted
@@ -336,7 +352,17 @@ class MailboxReduceScatterFedAvg:
                            lambda ver: self._key(ver, 0, k))
         absent = sorted(p for p in self.peers if p not in got)
         rejoined = sorted(p for p in self.peers if p in self.dead and p in got)
-        self.dead = set(absent)
+        # an absent rank whose newest post advanced is alive but lagging: it is waited on
+        # (bounded) again next round, which lets it catch up to the federation's epoch
+        lagging = []
+        for p, h in self.rs.headers(absent).items():
+            nw = self.rs.newest(h)
+            if nw is not None and nw[1].version > self.last_seen[p]:
+                lagging.append(p)
+                self.last_seen[p] = int(nw[1].version)
+        for p, sn in got.items():
+            self.last_seen[p] = max(self.last_seen[p], int(sn.version))
+        self.dead = set(absent) - set(lagging)
         live = sorted([k] + list(got))
         a0 = k * self.shard
         gk = self.gsend[slot]
@@ -354,8 +380,11 @@ class MailboxReduceScatterFedAvg:
         # ---- 3. all-gather: every owner's G shard to every rank ------------------------------------
         self._post(self.ag, gk, Snapshot(v, r, _f2i(wsum), self.shard * 4, b"\0" * 32, mask),
                    self.peers, self._key(v, 1, -1))
+        # owners absent from this round's reduce (dead or lagging) are only checked, never
+        # waited on: a dead owner would otherwise cost the full timeout every round
         owners = self._gather(self.ag, {p: v for p in self.peers}, self.stage_ag,
-                              [p for p in self.peers], lambda ver: self._key(ver, 1, -1))
+                              [p for p in self.peers if p not in absent],
+                              lambda ver: self._key(ver, 1, -1))
         out = torch.empty_like(partial)
         absent_owners = []
         for q in range(W):
@@ -381,7 +410,7 @@ class MailboxReduceScatterFedAvg:
         return out, {"live_ranks": live, "absent_ranks": absent, "live_weight": wsum,
                      "rejoined_ranks": rejoined, "view_mismatch": mismatch,
                      "absent_owners": absent_owners, "wait_s": time.perf_counter() - t_start,
-                     "epoch": v, "epochs_skipped": 0, "bytes_sent": float(sent)}
+                     "epoch": v, "epochs_skipped": skipped, "bytes_sent": float(sent)}
 
     def take_records(self) -> List[dict]:
         out, self.records = self.records, []

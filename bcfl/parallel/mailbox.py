@@ -288,8 +288,11 @@ class MailboxTransport:
             self.bytes_posted += self.payload_bytes
         if evs:
             # extend, not replace: per-destination posts of one version (post_to) each add the
-            # events of their copies, and the slot is free only after all of them
-            self.posted.setdefault((c, slot), []).extend(evs)
+            # events of their copies, and the slot is free only after all of them. Events that
+            # have completed are dropped here, so a caller that never calls wait_slot_free (the
+            # information-passing measurement) does not grow the list without bound
+            keep = [e for e in self.posted.get((c, slot), []) if not e.query()]
+            self.posted[(c, slot)] = keep + evs
 
     def _collect_timings(self):
         keep = []

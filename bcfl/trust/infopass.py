@@ -99,7 +99,9 @@ def measure(numel: int, sources: Optional[Sequence[int]] = None, iters: int = 3,
                    root if torch.is_tensor(root) else None)
         if tr.is_cuda:
             cur = torch.cuda.current_stream(dev)
-            for ev in tr.posted.get((me, v % 2), []):
+            # pop: the current stream waits for these copies, so the slot needs no later wait
+            # (and the events of past measurements do not pile up in the transport)
+            for ev in tr.posted.pop((me, v % 2), []):
                 cur.wait_event(ev)
 
     def commit():

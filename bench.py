@@ -373,6 +373,7 @@ def main():
                 "each rank's first client model on the draw (rank 0 reported)"),
             "final_majority_rate": last.get("global_majority_rate"),
             "accuracy_curve": [round(float(x), 4) for x in fed.global_accuracies],
+            "accuracy_curve_rounds": list(fed.global_accuracy_rounds),
             "accuracy_curve_scope": "rank 0's hosted client models on their strides of the draw, per round",
             "global_eval_rows": last.get("global_eval_rows"),
             "final_train_loss": last.get("train_loss"),

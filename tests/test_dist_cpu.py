@@ -253,6 +253,10 @@ def _bench_path_worker(rank, world, out, kw):
         res["audit_mismatched"] = torch.tensor(fed.ledger_audit["mismatched"])
     if not fed.collective_free:
         res["consensus"] = torch.tensor(fed.ledger.consensus_check())
+    import json as _json
+    res["verdicts"] = sorted((_json.loads(b["payload"])["src_round"], b["client"], b["verdict"])
+                             for b in fed.ledger.blocks() if b["kind"] == "verdict")
+    res["collective_free"] = bool(fed.collective_free)
     return res
 
 
@@ -270,12 +274,20 @@ def test_bench_path_world8_mailbox(tmp_path):
 
 @pytest.mark.slow
 def test_bench_path_world8_anomaly_filter_consensus(tmp_path):
-    """Same on 8 ranks with the update anomaly filter on (collective rounds): the hash-chained
-    ledger is identical on every rank after every round (consensus_check)."""
+    """Same on 8 ranks with the update anomaly filter on. Round 6: the filter runs inside the
+    asynchronous round-complete application (no collective), so every rank keeps its own chain —
+    and every rank reaches the SAME verdict on every source of every complete round it applied
+    (each judges identical payloads), every accepted update matches its sender's commitment."""
     res = run_world(_bench_path_worker, 8, str(tmp_path / "d"), str(tmp_path / "d"),
                     {"anomaly_filter": "both", "wire_dtype": "bf16"})
-    assert all(bool(r["consensus"]) for r in res)
-    assert len({r["tip"] for r in res}) == 1
+    for r in res:
+        assert r["collective_free"]
+        assert int(r["audit_checked"]) > 0 and int(r["audit_mismatched"]) == 0
+    rounds = set.intersection(*[{t for t, _, _ in r["verdicts"]} for r in res])
+    assert rounds, "no complete round was judged on every rank"
+    views = [[v for v in r["verdicts"] if v[0] in rounds] for r in res]
+    assert all(v == views[0] for v in views)
+    assert len(views[0]) == 8 * len(rounds)   # one verdict per source per judged round
 
 
 def _server_liveness_worker(rank, world, out, exit_after):
@@ -321,13 +333,13 @@ def test_server_mailbox_equals_allreduce_when_all_live(tmp_path):
     torch.testing.assert_close(a[0]["master"], b[0]["master"], atol=1e-6, rtol=0)
 
 
-def _server_lagging_worker(rank, world, out, join_after):
+def _server_lagging_worker(rank, world, out, join_after, transport="mailbox"):
     import json as _json
     import time as _time
     from bcfl.fl import Federation
     # the deadline only has to separate "not started yet" (rank 1 waits on a flag) from a live
     # rank on a loaded CPU (parallel test workers): 1 s was flaky there, 4 s is not
-    fed = Federation(_cfg("server", out, num_clients=2, num_rounds=10, server_transport="mailbox",
+    fed = Federation(_cfg("server", out, num_clients=2, num_rounds=10, server_transport=transport,
                           server_timeout_s=4.0), verbose=False)
     go, joined = os.path.join(out, "rank0_alone.flag"), os.path.join(out, "rank1_joined.flag")
 
@@ -365,15 +377,18 @@ def _server_lagging_worker(rank, world, out, join_after):
             "audit_mismatched": torch.tensor(fed.ledger_audit["mismatched"])}
 
 
-def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path):
+@pytest.mark.parametrize("transport", ["mailbox", "mailbox_rs"])
+def test_server_mailbox_slow_rank_rejoins_and_split_is_flagged(tmp_path, transport):
     """ADVICE r3 / VERDICT r4 #3: a rank that misses deadlines (slow, not dead) must not be excluded
     for good, must not report the epochs it skipped as trained, and a split must never be silent.
     Rank 1 joins only after rank 0 has aggregated 3 epochs alone (gated on rank 0's rounds, not on
     sleeps): rank 1 joins the federation's current epoch and records the skipped ones; the split
     of that epoch is reported (view_mismatch); rank 0 waits for rank 1 again; at the end every
     rank's final global-model root is compared (ledger ``final_check``) — equal models, or a
-    split flagged on every rank."""
-    res = run_world(_server_lagging_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), 3)
+    split flagged on every rank. Both mailbox transports (the reduce-scatter path now
+    takes the same epoch catch-up rule and waits for a lagging rank again)."""
+    res = run_world(_server_lagging_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), 3,
+                    transport)
     r0, r1 = res
     assert r0["absent"][0] == [1]                      # rank 0 timed out on the late rank 1
     assert r1["absent"][0] == []                       # ... which joined rank 0's epoch
@@ -419,6 +434,7 @@ def _rs_dead_worker(rank, world, out):
     fed.finish(audit=False)
     return {"rounds": torch.tensor(len(fed.history)), "G": fed.global_master.clone(),
             "live_w": torch.tensor([h["live_weight"] for h in fed.history], dtype=torch.float64),
+            "wait": torch.tensor([h["wait_s"] for h in fed.history], dtype=torch.float64),
             "absent": [list(h.get("absent_ranks", [])) for h in fed.history]}
 
 
@@ -433,6 +449,9 @@ def test_server_mailbox_reduce_scatter_survives_a_dead_rank(tmp_path):
         assert r["live_w"].tolist()[:2] == pytest.approx([1.0, 1.0])
         assert r["live_w"].tolist()[2:] == pytest.approx([2 / 3, 2 / 3])
         assert r["absent"][2:] == [[2], [2]]
+        # the dead rank costs ONE timeout (round 2, where it is still counted live);
+        # afterwards its reduce shard and its owner shard are only checked, never waited on
+        assert float(r["wait"][3]) < 5.0, r["wait"].tolist()
 
 
 @pytest.mark.slow
@@ -454,3 +473,43 @@ def test_server_world8_allreduce_equals_mailbox_fedavg(tmp_path):
         assert torch.equal(c[r]["master"], c[0]["master"])
     torch.testing.assert_close(b[0]["master"], a[0]["master"], atol=1e-6, rtol=0)
     torch.testing.assert_close(c[0]["master"], a[0]["master"], atol=2e-4, rtol=0)
+
+
+def _global_avg_worker(rank, world, out, kw):
+    import numpy as _np
+    from bcfl.ckpt import hf_layout, read_safetensors
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    fed = Federation(_cfg("serverless", out, **kw), verbose=False)
+    fed.run()
+    mine = torch.stack([fed.client_master[c] for c in fed.local_clients]) if fed.multi \
+        else fed.flat.master.clone()[None]
+    allm = D.all_gather_object(mine)
+    res = {"models": torch.cat(allm)}
+    if rank == 0:
+        sd = read_safetensors(os.path.join(out, "global", "model.safetensors"))
+        vec = torch.full((fed.flat.numel,), float("nan"))
+        for name, off, shape in hf_layout(fed.model, fed.flat):
+            vec[off:off + int(_np.prod(shape))] = sd[name].reshape(-1).float()
+        res["global"] = vec
+    return res
+
+
+@pytest.mark.parametrize("transport", ["mailbox", "rccl"])
+def test_serverless_global_checkpoint_is_the_mean_world2(tmp_path, transport):
+    """VERDICT r5 #4 on 2 ranks x 2 clients: ``global/model.safetensors`` == the mean of ALL four
+    client masters (fp32, atol 1e-6) — through one all-reduce in lock-step mode, and under the
+    collective-free round-complete protocol because every client model at a round end IS the
+    federation mean of the complete rounds (the final round closes synchronously)."""
+    kw = {"num_clients": 4, "num_rounds": 3, "save_every": 1, "ledger": False}
+    if transport == "rccl":
+        kw.update(async_gossip=False, gossip_transport="rccl", topology="ring")
+    else:
+        kw.update(gossip_transport="mailbox")
+    res = run_world(_global_avg_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"), kw)
+    models = res[0]["models"]
+    assert models.shape[0] == 4
+    g = res[0]["global"]
+    cov = ~torch.isnan(g)          # the flat buffer's alignment padding is in no HF tensor
+    assert float(cov.float().mean()) > 0.99
+    torch.testing.assert_close(g[cov], models.mean(0)[cov], atol=1e-6, rtol=0)

@@ -93,10 +93,14 @@ def test_checkpoint_roundtrip_and_hf_load(tmp_out):
     assert len(sd) == len(fed.model.hf_state_dict())
     hf = transformers.AutoModelForSequenceClassification.from_pretrained(gdir)
     assert type(hf).__name__ == "BertForSequenceClassification"
-    ours = fed.model.hf_state_dict()
-    for k, v in hf.state_dict().items():
-        if k in ours:
-            torch.testing.assert_close(v, ours[k].float())
+    # the saved global model is the mean of the client models (reference avg_params)
+    from bcfl.ckpt import hf_layout
+    mean = torch.stack([fed.client_master[c] for c in fed.local_clients]).mean(0)
+    lay = {n: (o, s) for n, o, s in hf_layout(fed.model, fed.flat)}
+    hsd = hf.state_dict()
+    for k, (o, shp) in lay.items():
+        torch.testing.assert_close(hsd[k], mean[o:o + int(np.prod(shp))].reshape(shp),
+                                   atol=1e-6, rtol=0)
     st = json.load(open(os.path.join(gdir, "state.json")))
     assert st["round"] == 1
     # ledger + metrics artefacts
@@ -516,3 +520,97 @@ def test_uniform_gossip_mix_shared_sum_matches_per_client(tmp_path, monkeypatch)
     assert getattr(a.gossip, "_mix_sum", None) is not None and getattr(b.gossip, "_mix_sum", None) is None
     for c in a.local_clients:
         torch.testing.assert_close(a.client_master[c], b.client_master[c], atol=1e-4, rtol=1e-4)
+
+
+def _global_flat(fed, out_dir):
+    """<out>/global/model.safetensors as a flat fp32 vector in the federation's layout."""
+    from bcfl.ckpt import hf_layout, read_safetensors
+    sd = read_safetensors(os.path.join(out_dir, "global", "model.safetensors"))
+    vec = torch.full((fed.flat.numel,), float("nan"))
+    for name, off, shape in hf_layout(fed.model, fed.flat):
+        vec[off:off + int(np.prod(shape))] = sd[name].reshape(-1).float()
+    return vec
+
+
+@pytest.mark.parametrize("transport", ["rccl", "loopback"])
+def test_serverless_global_checkpoint_is_the_federation_mean(tmp_out, transport):
+    """the serverless ``global/`` checkpoint is the unweighted mean of the client
+    models, as the reference saves ``avg_params`` (serverless_NonIID_IMDB.py:296-297,305), not one
+    client's model — checked on a ring (lock-step, the client models differ) and on the
+    asynchronous loopback protocol; state.json scores the saved model itself."""
+    kw = dict(mode="serverless", num_clients=4, num_rounds=2, save_every=1, ledger=False)
+    if transport == "rccl":
+        kw.update(async_gossip=False, gossip_transport="rccl", topology="ring")
+    else:
+        kw.update(gossip_transport="loopback")
+    fed = Federation(_cfg(tmp_out, **kw), verbose=False)
+    fed.run()
+    masters = torch.stack([fed.client_master[c] for c in range(4)])
+    mean = masters.mean(0)
+    g = _global_flat(fed, tmp_out)
+    cov = ~torch.isnan(g)          # the flat buffer's alignment padding is in no HF tensor
+    assert float(cov.float().mean()) > 0.99
+    torch.testing.assert_close(g[cov], mean[cov], atol=1e-6, rtol=0)
+    if transport == "rccl":   # the ring's client models really differ: not any one of them
+        assert float((masters[0] - mean).abs().max()) > 1e-5
+    st = json.load(open(os.path.join(tmp_out, "global", "state.json")))
+    assert "mean of all 4 client models" in st["global_model"]
+    assert 0.0 <= float(st["global_model_accuracy"]) <= 1.0
+    assert st["global_accuracy_rounds"] == [0, 1]
+
+
+def test_loopback_async_filter_rejects_byzantine_every_round(tmp_out):
+    """The asynchronous trust pipeline at N = 1 (every client its own virtual rank, posts landing
+    1-2 local steps late, mid-round application on): each complete round is judged before it is
+    applied, the 50x-scaled client is rejected in every round, and no model — its own included —
+    ever holds its update (all four end on the same honest consensus)."""
+    fed = Federation(_cfg(tmp_out, mode="serverless", num_clients=4, num_rounds=4,
+                          gossip_transport="loopback", anomaly_filter="both",
+                          inject_byzantine={1: 50.0}, save_every=0), verbose=False)
+    assert fed._gossip_filter and fed.gossip.apply_on_arrival and fed.collective_free
+    fed.run()
+    judged = [tuple(x) for h in fed.history for x in h.get("verdict_rounds", [])]
+    assert [t for t, _ in judged] == [0, 1, 2, 3], judged
+    assert all(list(rej) == [1] for _, rej in judged), judged
+    rej_blocks = {(json.loads(b["payload"])["src_round"], b["client"]) for b in fed.ledger.blocks()
+                  if b["kind"] == "verdict" and b["verdict"] != "accept"}
+    assert rej_blocks == {(t, 1) for t in range(4)}
+    m = torch.stack([fed.client_master[c] for c in range(4)])
+    assert torch.isfinite(m).all()
+    for c in range(1, 4):
+        torch.testing.assert_close(m[c], m[0], atol=1e-6, rtol=0)
+
+
+def test_server_holdout_gate_keeps_previous_global_model(tmp_out):
+    """Server hold-out selection: a new global model scoring more than ``server_holdout_tol``
+    below the best on the server's validation slice (train rows no client uses) is not adopted —
+    the next round starts from the previous global model — and after ``server_holdout_patience``
+    rejections in a row the next result is adopted anyway. A tolerance of -1 rejects every model
+    after the first, so the pattern is: adopt, reject, reject, adopt (patience)."""
+    fed = Federation(_cfg(tmp_out, mode="server", num_rounds=4, save_every=0, ledger=True,
+                          partition="iid_random", server_holdout=24, server_holdout_tol=-1.0,
+                          server_holdout_patience=2, keep_optimizer_state=True), verbose=False)
+    rows = fed._holdout_rows()
+    used = {int(i) for sp in fed.partitions(0) for i in sp.train}
+    assert len(rows) == 24 and not (set(int(i) for i in rows) & used)
+    fed.run()
+    assert [h["holdout_adopted"] for h in fed.history] == [True, False, False, True]
+    roots = [b["update_root"] for b in fed.ledger.blocks() if b["kind"] == "global"]
+    assert roots[1] == roots[0] and roots[2] == roots[0] and roots[3] != roots[0]
+    assert all(0.0 <= h["holdout_acc"] <= 1.0 for h in fed.history)
+
+
+def test_server_holdout_rejection_restores_client_optimizer_states(tmp_out):
+    """A rejected round is undone completely: the clients' kept AdamW moments are the ones from
+    before the round (patience 0 = pure model selection: never forced)."""
+    fed = Federation(_cfg(tmp_out, mode="server", num_rounds=1, save_every=0, ledger=False,
+                          partition="iid_random", server_holdout=24, server_holdout_tol=-1.0,
+                          keep_optimizer_state=True), verbose=False)
+    fed.run_round(0)                                   # first result: always adopted
+    before = {c: {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
+              for c, st in fed.client_opt.items()}
+    fed.run_round(1)                                   # tol -1: rejected
+    assert fed.history[-1]["holdout_adopted"] is False
+    for c, st in fed.client_opt.items():
+        for k, v in before[c].items():
+            assert torch.equal(st[k], v), (c, k)

@@ -254,3 +254,24 @@ def test_gpu_server_lanes_close_to_sequential(tmp_path):
     assert torch.isfinite(b[0]).all()
     assert float((a[0] - b[0]).abs().max()) < 2e-4
     assert a[1] == pytest.approx(b[1], rel=1e-3)
+
+
+def test_gpu_lanes_run_has_no_unordered_stream_access(tmp_path, monkeypatch):
+    """the 3-lane federation (lanes on their own streams, the eval side stream,
+    the checkpoint copy stream) under the happens-before checker (BCFL_DEBUG_STREAMS): every
+    buffer one stream writes and another touches is ordered by an event — no race is reported."""
+    monkeypatch.setenv("BCFL_DEBUG_STREAMS", "1")
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    D.set_runtime_for_tests(None)
+    cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=4,
+                   num_rounds=2, train_samples=64, test_samples=32, global_test_samples=64,
+                   out_dir=str(tmp_path), reference_prints=False, client_lanes=3,
+                   overlap_wgrad=False, async_gossip=False, gossip_transport="rccl", ledger=True,
+                   save_every=1, dropout=0.1, drift_correction="scaffold")
+    fed = Federation(cfg, verbose=False)
+    fed.run()
+    D.set_runtime_for_tests(None)
+    assert fed.stream_races is not None, "the checker did not run"
+    assert fed.stream_races == [], "\n".join(fed.stream_races)

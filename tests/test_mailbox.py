@@ -2,6 +2,7 @@
 gloo for the one start-up handle exchange) of the hipIpc transport. Properties: posts need no
 matching receive, torn snapshots are rejected, tampered payloads fail the Merkle commitment and are
 recorded in the ledger, and a slow or EXITED peer never stalls the others."""
+import json
 import os
 import time
 
@@ -189,11 +190,10 @@ def _learn_worker(rank, world, out, kw):
     from bcfl.fl import Federation
     kw = dict(kw)
     torch.set_num_threads(kw.pop("threads", 2))
-    # cosine decay: at a constant 2e-3 the tiny model, once converged, is kicked around by every
-    # round's fresh-AdamW steps (8 ranks: ~1.0 by round 17, then 0.64-0.92 oscillations; with the
-    # decay 0.96-1.0 to the end)
-    base = dict(model="tiny-bert", num_clients=4, num_rounds=16, mode="serverless", lr=2e-3,
-                lr_schedule="cosine", lr_warmup_steps=8, max_seq_len=64, train_samples=256, global_test_samples=200,
+    # the preset's recipe (warm-up, then a constant rate, as the bench runs it); only the tiny
+    # model's learning rate and the run's shape are the test's own
+    base = dict(model="tiny-bert", num_clients=4, num_rounds=16, mode="serverless", lr=1e-3,
+                max_seq_len=64, train_samples=256, global_test_samples=200,
                 eval_local=False, save_every=0, ledger=False, device="cpu",
                 reference_prints=False, out_dir=out, backend="gloo", gossip_transport="mailbox")
     base.update(kw)
@@ -247,15 +247,17 @@ def test_mailbox_async_two_ranks_slow_peer_default_protocol(tmp_path):
 
 @pytest.mark.slow
 def test_mailbox_async_four_ranks_learn_label_shards(tmp_path):
-    """Same with one client per rank (every neighbour remote: every mix is stale). Both tests run
-    UNBOUNDED (gossip_max_lead = 0: no rank ever waits); the default bound is pinned below.
-    Unbounded, one client per rank learns but is the least stable regime (ranks run at their own
-    pace, a round completes whenever its last post lands): every rank reaches 0.9 within the last
-    10 rounds and the federation ends >= 0.75 (final 0.83-0.96 over 5 runs here); the bounded
-    default holds >= 0.9 to the end (eight-rank test below)."""
+    """One client per rank (every neighbour remote: every application is of posts that crossed
+    the transport) with the DEFAULT protocol: round-complete application, bounded staleness 1,
+    round-tagged corrections. (Unbounded staleness, gossip_max_lead = 0, is not a supported
+    learning regime for one client per rank: ranks run at their own pace and a round completes
+    whenever its last post lands; round 5 measured 0.83-0.96 final accuracy over 5 runs.)"""
     res = run_world(_learn_worker, 4, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"num_rounds": 30, "liveness_timeout": 6, "gossip_max_lead": 0})
-    _check_async_learning(res, last=10, final=0.75)
+                    {"num_rounds": 24})
+    for r in res:
+        assert not r["same_round"] and r["exchange"] and r["delta"]
+        assert float(r["acc"][-3:].max()) >= 0.9 - 1e-6, r["acc"].tolist()
+        assert float(r["fa"]["accuracy"]) >= 0.9 - 1e-6, r["fa"]
 
 
 @pytest.mark.slow
@@ -317,21 +319,33 @@ def _byz_worker(rank, world, out, kw):
     fed = Federation(_cfg(out, **kw), verbose=False)
     fed.run()
     g = fed.gossip
-    return {"rejected": [list(h["rejected"]) for h in fed.history],
+    judged = [tuple(x) for h in fed.history for x in h.get("verdict_rounds", [])]
+    blocks = [b for b in fed.ledger.blocks() if b["kind"] == "verdict"]
+    return {"judged": judged,
+            "ledger_rejects": sorted({(json.loads(b["payload"])["src_round"], b["client"])
+                                      for b in blocks if b["verdict"] != "accept"}),
             "delta": torch.tensor(int(g.exchange == "delta")),
             "arrival": torch.tensor(int(g.apply_on_arrival)),
+            "models": torch.stack([fed.client_master[c] for c in fed.local_clients]),
             "finite": torch.tensor(int(torch.isfinite(fed.flat.master).all()))}
 
 
 def test_mailbox_delta_exchange_anomaly_filter_rejects_byzantine(tmp_path):
-    """the update anomaly filter under the DEFAULT multi-rank exchange (delta,
-    2 ranks x 2 clients). A client whose update is scaled 50x is rejected every round, and only
-    it: every client's sketch and norm are measured from the gossip's round-start record, so an
-    honest client's statistics never carry a neighbour's (Byzantine) update, and mid-round
-    application is off while verdicts are in play."""
+    """the update anomaly filter runs INSIDE the asynchronous round-complete
+    protocol, with mid-round application ON (2 ranks x 2 clients, modified Z + PageRank). Each
+    receiver judges a complete round's updates (sketch + norm of S_j^T - S_j^applied, measured on
+    what it is about to apply) before applying any of them, so the client whose update is scaled
+    50x is rejected in EVERY round, by every rank, with no collective and no previous-round
+    verdicts, and its update never enters any model — its own included: every client model on
+    both ranks ends on the same honest consensus."""
     res = run_world(_byz_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"num_clients": 4, "num_rounds": 4, "anomaly_filter": "modz",
+                    {"num_clients": 4, "num_rounds": 4, "anomaly_filter": "both",
                      "inject_byzantine": {1: 50.0}})
     for r in res:
-        assert int(r["delta"]) == 1 and int(r["arrival"]) == 0 and int(r["finite"]) == 1
-        assert all(rej == [1] for rej in r["rejected"]), r["rejected"]
+        assert int(r["delta"]) == 1 and int(r["arrival"]) == 1 and int(r["finite"]) == 1
+        assert [t for t, _ in r["judged"]] == [0, 1, 2, 3], r["judged"]
+        assert all(list(rej) == [1] for _, rej in r["judged"]), r["judged"]
+        assert r["ledger_rejects"] == [(t, 1) for t in range(4)]
+    models = torch.cat([r["models"] for r in res])
+    for m in models[1:]:
+        torch.testing.assert_close(m, models[0], atol=1e-5, rtol=0)

@@ -190,3 +190,28 @@ def test_info_passing_mailbox_gloo(tmp_path):
     # all three reference detectors, each with its own re-measured rows (or the skip reason)
     assert r["dets"] == ["dbscan", "modz", "pagerank"] and r["det_rows"] == 9
     assert r["lines"] == 3 + 9
+
+
+def test_update_filter_non_finite_and_mad_floor():
+    """Round 6: a non-finite update is always rejected (whatever the majority rule), the rest are
+    judged on their own; near-equal honest norms (tiny MAD) or two classes' norms 2x apart do not
+    get an honest client rejected, a 50x boost does."""
+    import numpy as np
+    from bcfl.trust.anomaly import UpdateAnomalyFilter
+    rng = np.random.default_rng(0)
+    base = rng.standard_normal(64)
+    sk = np.stack([base + 0.05 * rng.standard_normal(64) for _ in range(8)])
+    f = UpdateAnomalyFilter("both")
+    # honest: norms within a few percent, one 15 % lower (MAD ~1 %: plain modified Z says reject)
+    norms = np.array([0.55, 0.56, 0.55, 0.57, 0.56, 0.55, 0.47, 0.56])
+    assert f(sk, norms).rejected == set()
+    # label-shard classes 2x apart, 3 vs 4 clients
+    assert f(sk[:7], np.array([1.0, 1.1, 1.05, 0.45, 0.44, 0.46, 0.45])).rejected == set()
+    # boosted client 3
+    v = f(sk, np.array([0.55, 0.56, 0.55, 27.5, 0.56, 0.55, 0.57, 0.56]))
+    assert v.rejected == {3} and v.reasons[3] == "modz"
+    # non-finite client 5 (plus the boosted 3): both rejected, reasons kept
+    sk2 = sk.copy()
+    sk2[5, 0] = np.nan
+    v = f(sk2, np.array([0.55, 0.56, 0.55, 27.5, 0.56, np.nan, 0.57, 0.56]))
+    assert v.rejected == {3, 5} and v.reasons[5] == "non-finite"
