@@ -164,6 +164,10 @@ class FLConfig:
     #                                     is not adopted (the previous global model is kept for the
     #                                     next round) — 0 = off (Flower FedAvg adopts every result)
     server_holdout_tol: float = 0.05
+    server_holdout_min: float = 0.9     # the gate engages once the best adopted hold-out accuracy
+    #                                     reaches this (early rounds pass a plateau through dips
+    #                                     that selection would freeze: server, 5 clients, gated
+    #                                     from round 0: stuck at 0.686 for 10 rounds)
     server_holdout_patience: int = 0    # > 0: after this many rejections in a row the next result
     #                                     is adopted anyway; 0: pure model selection (a rejected
     #                                     round is undone — global model and the clients' kept

@@ -495,9 +495,13 @@ class EvalMixin:
         best = getattr(self, "_holdout_best", -1.0)
         streak = getattr(self, "_holdout_streak", 0)
         pat = int(cfg.server_holdout_patience)
-        adopt = acc >= best - float(cfg.server_holdout_tol) or (pat > 0 and streak >= pat)
+        gated = best >= float(cfg.server_holdout_min)
+        adopt = (not gated or acc >= best - float(cfg.server_holdout_tol)
+                 or (pat > 0 and streak >= pat))
         if adopt:
-            self._holdout_best = max(best, acc)
+            # ungated (before the best reaches server_holdout_min) the best follows the adopted
+            # models; gated it only rises
+            self._holdout_best = max(best, acc) if gated else acc
             self._holdout_streak = 0
         else:
             self._holdout_streak = streak + 1

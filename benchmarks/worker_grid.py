@@ -38,14 +38,26 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
                      reference_prints=False, save_every=1, keep_optimizer_state=keep_opt,
                      **extra)
     fed = Federation(cfg, verbose=False)
+    # steady-state time as bench.py measures it: the rounds after the first 3 as ONE block,
+    # synchronised only at its two ends (a per-round device sync would serialise every round's
+    # host-side start with the GPU and penalise the protocol that defers its host reads)
+    warm = 3 if rounds > 4 else 0
     times = []
+    t_block = None
     for r in range(rounds):
+        if r == warm:
+            if fed.is_cuda:
+                torch.cuda.synchronize()
+            t_block = time.perf_counter()
         t0 = time.perf_counter()
         fed.run_round(r)
-        if fed.is_cuda:
-            torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     fed.drain()
+    if fed.ckpt is not None:
+        fed.ckpt.wait()
+    if fed.is_cuda:
+        torch.cuda.synchronize()
+    steady_s = (time.perf_counter() - t_block) / max(rounds - warm, 1)
     fed.timer.resolve(block=True)
     steady_h = fed.history[3:] if len(fed.history) > 4 else fed.history
     phases = {}
@@ -55,11 +67,11 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
                 phases[k] = phases.get(k, 0.0) + float(v) / len(steady_h)
     fa = fed.federation_accuracy()
     fed.finish()
-    steady = times[3:] if len(times) > 4 else times
     rec = {"mode": mode, "clients": clients, "rounds": rounds, "model": model,
            "keep_optimizer_state": keep_opt, "overrides": extra,
            "train_loss_curve": [h.get("train_loss") for h in fed.history],
-           "s_per_round_steady": sum(steady) / len(steady), "total_rounds_s": sum(times),
+           "s_per_round_steady": steady_s, "host_issue_s_per_round": times,
+           "total_rounds_s": sum(times),
            "process_latency_min": (time.time() - t_proc) / 60.0,
            "final_accuracy": fa.get("accuracy"), "global_eval_rows": fa.get("rows"),
            "final_majority_rate": fed.history[-1].get("global_majority_rate"),

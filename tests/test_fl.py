@@ -589,7 +589,8 @@ def test_server_holdout_gate_keeps_previous_global_model(tmp_out):
     after the first, so the pattern is: adopt, reject, reject, adopt (patience)."""
     fed = Federation(_cfg(tmp_out, mode="server", num_rounds=4, save_every=0, ledger=True,
                           partition="iid_random", server_holdout=24, server_holdout_tol=-1.0,
-                          server_holdout_patience=2, keep_optimizer_state=True), verbose=False)
+                          server_holdout_patience=2, server_holdout_min=0.0,
+                          keep_optimizer_state=True), verbose=False)
     rows = fed._holdout_rows()
     used = {int(i) for sp in fed.partitions(0) for i in sp.train}
     assert len(rows) == 24 and not (set(int(i) for i in rows) & used)
@@ -605,7 +606,7 @@ def test_server_holdout_rejection_restores_client_optimizer_states(tmp_out):
     before the round (patience 0 = pure model selection: never forced)."""
     fed = Federation(_cfg(tmp_out, mode="server", num_rounds=1, save_every=0, ledger=False,
                           partition="iid_random", server_holdout=24, server_holdout_tol=-1.0,
-                          keep_optimizer_state=True), verbose=False)
+                          server_holdout_min=0.0, keep_optimizer_state=True), verbose=False)
     fed.run_round(0)                                   # first result: always adopted
     before = {c: {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
               for c, st in fed.client_opt.items()}

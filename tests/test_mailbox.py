@@ -192,7 +192,7 @@ def _learn_worker(rank, world, out, kw):
     torch.set_num_threads(kw.pop("threads", 2))
     # the preset's recipe (warm-up, then a constant rate, as the bench runs it); only the tiny
     # model's learning rate and the run's shape are the test's own
-    base = dict(model="tiny-bert", num_clients=4, num_rounds=16, mode="serverless", lr=1e-3,
+    base = dict(model="tiny-bert", num_clients=4, num_rounds=16, mode="serverless", lr=6e-4,
                 max_seq_len=64, train_samples=256, global_test_samples=200,
                 eval_local=False, save_every=0, ledger=False, device="cpu",
                 reference_prints=False, out_dir=out, backend="gloo", gossip_transport="mailbox")
