@@ -36,7 +36,7 @@ class CheckpointMixin:
         self.provenance_rows += sum(len(sp.train) for sp in self.partitions(r))
 
     @torch.no_grad()
-    def _global_model(self) -> tuple:
+    def _global_model(self, r: int = -1) -> tuple:
         """(fp32 flat buffer, scope) of the model saved as ``<out>/global`` — the federation's
         model, as the reference saves it (serverless: ``avg_params`` = the unweighted mean of the
         client models, ``serverless_NonIID_IMDB.py:296-297,305``).
@@ -60,6 +60,9 @@ class CheckpointMixin:
         n_all = cfg.num_clients
         if len(srcs) == 1 and not self.rt.distributed:
             return srcs[0], "the only client model"
+        if self._average_eval() and getattr(self, "_avg_round", None) == r:
+            # global_eval_models='average' already built (and scored) this round's mean
+            return self._avg_master, f"mean of all {n_all} client models (the scored global model)"
         if not hasattr(self, "_save_avg"):
             self._save_avg = torch.empty_like(self.flat.master)
         avg = self._save_avg
@@ -90,7 +93,7 @@ class CheckpointMixin:
         gsrc = None
         if self.rt.distributed and not self.collective_free and cfg.mode == "serverless":
             # the lock-step mean is a collective: every rank, before any rank-local skip below
-            gsrc = self._global_model()
+            gsrc = self._global_model(r)
         pend = self._eval_pending
         if pend is not None and pend[0] == r and not self.collective_free and self.rt.distributed:
             # multi-rank collective mode: the saved accuracy is the job's (all-reduced), so
@@ -122,7 +125,7 @@ class CheckpointMixin:
             jobs = []
             scored = False
             if self.rt.is_main:
-                src, scope = gsrc if gsrc is not None else self._global_model()
+                src, scope = gsrc if gsrc is not None else self._global_model(r)
                 state["global_model"] = scope
                 if cfg.mode == "serverless" and self.multi and not self._hosted_models_identical() \
                         and not self._average_eval() and src is not self.flat.master:

@@ -115,6 +115,7 @@ class EvalMixin:
             return [(c, self.global_test_batches(r, c)) for c in self.local_clients]
         if self._average_eval():
             self._refresh_average()
+            self._avg_round = r
             return [(-1, self.global_test_batches(r))]
         return [(None, self.global_test_batches(r))]
 
@@ -430,10 +431,11 @@ class EvalMixin:
     @torch.no_grad()
     def _score_async(self, master: torch.Tensor, r: int):
         """Accuracy of an fp32 model on round r's whole global draw, queued on the evaluation side
-        stream (a bf16 snapshot taken there first, so ``master`` may be overwritten as soon as the
-        training stream has waited for the copy). Returns a function that waits for the result —
-        called by the checkpoint writer thread, never by the training loop. Without a side stream
-        (CPU) the model is scored inline."""
+        stream. The bf16 snapshot is taken on the TRAINING stream (one cast pass; ``master`` may be
+        overwritten right after it), so the training stream never waits behind the round's
+        global evaluation already queued on the side stream. Returns a function that waits for
+        the result — called by the checkpoint writer thread, never by the training loop. Without
+        a side stream (CPU) the model is scored inline."""
         if self.eval_stream is None:
             acc = self._score_model(master, r)
             return lambda: acc
@@ -445,18 +447,19 @@ class EvalMixin:
             pad_multiple=self.pad_multiple).device_batches(self.device))
         if not hasattr(self, "_score_snap"):
             self._score_snap = torch.empty(self.flat.numel, dtype=self.flat.dtype, device=self.device)
-        es.wait_stream(main)                       # the mean and the batches are ready
+            self._score_done = None
+        if self._score_done is not None:
+            main.wait_event(self._score_done)      # the previous save round's scoring read it
+        ops.cast_copy_(self._score_snap, master)
+        es.wait_stream(main)                       # the snapshot and the batches are ready
         own = self.eval_flat.param
         with torch.cuda.stream(es):
-            ops.cast_copy_(self._score_snap, master)
-            copied = torch.cuda.Event()
-            copied.record(es)
             self.eval_flat.rebind(self.eval_flat.master, self._score_snap)
             stats = self.eval_trainer.evaluate_device(gb)
             done = torch.cuda.Event()
             done.record(es)
         self.eval_flat.rebind(self.eval_flat.master, own)
-        main.wait_event(copied)                    # later writers of `master` come after the copy
+        self._score_done = done
 
         def result(stats=stats, done=done, gb=gb):
             done.synchronize()

@@ -8,6 +8,7 @@ on the device so an epoch has exactly one host sync.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Sequence
 
@@ -37,6 +38,24 @@ class EvalResult:
     def ref_loss(self) -> float:
         """Reference ``test()``: Σ batch-mean losses ÷ dataset size."""
         return self.batch_mean_sum / max(self.count, 1)
+
+
+# Backward on the calling thread: autograd's per-device worker thread hands every Python
+# backward Function across threads (GIL hand-off per node), which made the one-client step's
+# host issue 8.1 ms against 9.6 ms of device time, and the device idled wherever the host fell
+# behind (loss head, optimizer launch, step boundary). On the caller thread the same step issues
+# in 5.8 ms (scripts/host_step_timing.py, profiles/host_issue_r6.json). Streams are unchanged:
+# each backward node still runs on the stream its forward ran on. BCFL_AUTOGRAD_THREAD=1 restores
+# the worker thread (A/B runs).
+_CALLER_THREAD_BACKWARD = os.environ.get("BCFL_AUTOGRAD_THREAD", "0") != "1"
+
+
+def backward(loss: torch.Tensor) -> None:
+    if _CALLER_THREAD_BACKWARD and loss.is_cuda:
+        with torch.autograd.set_multithreading_enabled(False):
+            loss.backward()
+    else:
+        loss.backward()
 
 
 class MicroReplica:
@@ -72,15 +91,15 @@ class LocalTrainer:
                 lb = ops.cross_entropy(rep.model(b), b.labels) * (b.batch_size / B)
         else:
             lb = ops.cross_entropy(rep.model(b), b.labels) * (b.batch_size / B)
-        la.backward()
+        backward(la)
         if main is not None:
             ops.join_wgrad(self.flat.device)
             with torch.cuda.stream(rep.stream):
-                lb.backward()
+                backward(lb)
                 ops.join_wgrad(self.flat.device)
             main.wait_stream(rep.stream)
         else:
-            lb.backward()
+            backward(lb)
         self.opt.step(partner=rep.flat)
         self.flat.zero_grad()
         rep.flat.zero_grad()
@@ -98,11 +117,11 @@ class LocalTrainer:
         if self.opt.overlap_active():
             # per-layer AdamW on a side stream, launched from the gradient hooks mid-backward
             self.opt.begin_overlapped()
-            loss.backward()
+            backward(loss)
             ops.join_wgrad(self.flat.device)
             self.opt.finish_overlapped()
         else:
-            loss.backward()
+            backward(loss)
             if self.flat.device.type == "cuda":
                 ops.join_wgrad(self.flat.device)  # overlapped weight gradients -> optimizer
             self.opt.step()

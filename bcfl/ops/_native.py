@@ -34,14 +34,21 @@ def _load():
     return _C
 
 
+_SC = None   # bcfl.utils.streamcheck, bound on first use (import cycle: utils imports ops)
+
+
 def native():
     """Return the extension module or raise (GPU path must never silently fall back)."""
-    m = _load()
+    global _SC
+    m = _C if _C is not None else _load()
     if m is None:
         raise RuntimeError("bcfl native extension unavailable on a GPU code path: " + str(_ERR))
-    from ..utils import streamcheck
-    if streamcheck.enabled():   # BCFL_DEBUG_STREAMS: every kernel call reported to the checker
-        return streamcheck.wrap_native(m)
+    sc = _SC
+    if sc is None:
+        from ..utils import streamcheck as sc
+        _SC = sc
+    if "det" in sc._STATE:   # BCFL_DEBUG_STREAMS: every kernel call reported to the checker
+        return sc.wrap_native(m)
     return m
 
 
@@ -49,20 +56,36 @@ def available() -> bool:
     return _load() is not None
 
 
+# The routing switches are read once per process (every op consults them: an os.environ lookup
+# per call was ~0.5 ms of host time per BERT-base step); code that changes them at run time
+# (tests, A/B drivers) calls refresh_env() afterwards.
+_FORCE = False
+_TORCH_OPS: frozenset = frozenset()
+
+
+def refresh_env() -> None:
+    global _FORCE, _TORCH_OPS
+    _FORCE = os.environ.get("BCFL_FORCE_TORCH", "0") == "1"
+    _TORCH_OPS = frozenset(filter(None, os.environ.get("BCFL_TORCH_OPS", "").split(",")))
+
+
+refresh_env()
+
+
 def force_torch() -> bool:
-    return os.environ.get("BCFL_FORCE_TORCH", "0") == "1"
+    return _FORCE
 
 
 def _torch_ops():
-    return set(filter(None, os.environ.get("BCFL_TORCH_OPS", "").split(",")))
+    return _TORCH_OPS
 
 
 def use_native(t, op: str = "") -> bool:
     """True when tensor ``t`` must go through the HIP kernels. ``BCFL_TORCH_OPS=attn,rope,...``
     routes the named ops to the reference path on GPU (bisection / A-B benchmarking only)."""
-    if not bool(getattr(t, "is_cuda", False)) or force_torch():
+    if _FORCE or not getattr(t, "is_cuda", False):
         return False
-    return not (op and op in _torch_ops())
+    return not (op and op in _TORCH_OPS)
 
 
 def load_error():

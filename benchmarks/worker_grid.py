@@ -32,6 +32,11 @@ def one(mode: str, clients: int, rounds: int, out_dir: str, model: str, keep_opt
     D.set_runtime_for_tests(None)
     t_proc = time.time()
     part = "shared_random" if mode == "server" else "iid_random"
+    if mode == "serverless":
+        # the reference's serverless global model: the mean of the client models, scored on the
+        # whole draw (serverless_IID_IMDB.py:269-279 avg_params -> global_model), as the server scores its
+        # FedAvg model: one model per round in both modes
+        extra.setdefault("global_eval_models", "average")
     cfg = get_preset("baseline3_learnable", mode=mode, model=model, num_clients=clients,
                      num_rounds=rounds, partition=part, train_samples=100, test_samples=100,
                      resample_each_round=(mode == "serverless"), out_dir=out_dir,

@@ -415,10 +415,11 @@ def _one_rank_run(tmp_path, tag, **kw):
     nt = torch.get_num_threads()
     torch.set_num_threads(2)
     try:
+        kw = {"save_every": 0, **kw}
         cfg = get_preset("baseline3_learnable", model="tiny-bert", num_clients=4, num_rounds=3,
                          mode="serverless", lr=2e-3, lr_warmup_steps=4, max_seq_len=64,
                          train_samples=64, global_test_samples=40, eval_local=False,
-                         save_every=0, ledger=False, device="cpu", reference_prints=False,
+                         ledger=False, device="cpu", reference_prints=False,
                          out_dir=str(tmp_path / tag), gossip_transport="mailbox",
                          wire_dtype="fp32", dropout=0.0, **kw)
         fed = Federation(cfg, verbose=False)
@@ -460,12 +461,28 @@ def test_global_eval_average_model_is_reference_global_model(tmp_path):
     on the whole draw — the reference serverless global_model (serverless_NonIID_IMDB.py:296-304)
     — while the default 'all' reports the mean client accuracy on disjoint strides."""
     import torch
+    import json
+    from safetensors.torch import load_file
     fed = _one_rank_run(tmp_path, "avg", global_eval_models="average", topology="ring",
-                        gossip_exchange="state")
+                        gossip_exchange="state", save_every=1)
     mean = torch.stack([fed.client_master[c] for c in range(4)]).mean(0)
     torch.testing.assert_close(fed._avg_master, mean, atol=1e-6, rtol=0)
     h = fed.history[-1]
     assert h["global_eval_rows"] == 40 and 0.0 <= h["global_acc"] <= 1.0
+    # the saved global/ model IS the scored average (no second mean pass, no second scoring)
+    fed.ckpt.wait()
+    gdir = tmp_path / "avg" / "global"
+    sd = load_file(str(gdir / "model.safetensors"))
+    ref = {}
+    fed.flat.load_master(mean)
+    for k, v in fed.model.state_dict().items():
+        ref[k] = v.float()
+    for k, v in sd.items():
+        if k in ref:
+            torch.testing.assert_close(v.float(), ref[k], atol=1e-6, rtol=0)
+    st = json.loads((gdir / "state.json").read_text())
+    assert "scored global model" in st["global_model"]
+    assert st["global_model_accuracy"] == st["global_accuracies"][-1] == h["global_acc"]
 
 
 def test_outer_optimizer_nesterov_and_heavy_ball():

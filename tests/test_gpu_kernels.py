@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from bcfl import ops
-from bcfl.ops import ref, rng
+from bcfl.ops import _native, ref, rng
 
 pytestmark = pytest.mark.gpu
 
@@ -506,6 +506,7 @@ def test_fused_ffn_autograd_matches_reference():
     res = {}
     for route in ("bcfl", "torch"):
         os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "gemm,gemm_act"
+        _native.refresh_env()
         try:
             x = x0.clone().requires_grad_(True)
             p1, q1, p2 = (t.clone().requires_grad_(True) for t in (w1, b1, w2))
@@ -516,6 +517,7 @@ def test_fused_ffn_autograd_matches_reference():
             res[route] = [y, x.grad, p1.grad, q1.grad, p2.grad]
         finally:
             os.environ["BCFL_TORCH_OPS"] = ""
+            _native.refresh_env()
     for name, a, b in zip(("y", "dx", "dW1", "db1", "dW2"), res["bcfl"], res["torch"]):
         # both sides are bf16 results of fp32 accumulations with different rounding points
         # (fused epilogue vs bf16 GEMM output + separate bias/GELU): compare normwise
@@ -541,6 +543,7 @@ def test_subset_attention_matches_torch_reference(nh, nkv, d, causal, p):
     res = {}
     for route in ("bcfl", "torch"):
         os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "subset_attn"
+        _native.refresh_env()
         try:
             ops.rng.global_rng().load_state({"seed": 5, "counter": 0})
             x = x0.clone().requires_grad_(True)
@@ -549,6 +552,7 @@ def test_subset_attention_matches_torch_reference(nh, nkv, d, causal, p):
             res[route] = (o.float(), x.grad.float())
         finally:
             os.environ["BCFL_TORCH_OPS"] = ""
+            _native.refresh_env()
     _close(res["bcfl"][0], res["torch"][0], 2e-2, 2e-2)
     _close(res["bcfl"][1], res["torch"][1], 2e-2, 2e-2)
 
@@ -559,11 +563,13 @@ def test_native_dropout_mask_matches_hash_layout():
     ops.rng.global_rng().load_state({"seed": 9, "counter": 4})
     y = ops.dropout(x, 0.1, True)
     os.environ["BCFL_TORCH_OPS"] = "dropout"
+    _native.refresh_env()
     try:
         ops.rng.global_rng().load_state({"seed": 9, "counter": 4})
         r = ops.dropout(x, 0.1, True)
     finally:
         os.environ["BCFL_TORCH_OPS"] = ""
+        _native.refresh_env()
     assert torch.equal(y == 0, r == 0)           # identical keep decisions
     _close(y, r, 1e-2, 1e-2)
 
@@ -589,6 +595,7 @@ def test_lora_linear_fused_matches_unfused(T, with_res):
     res = {}
     for route in ("bcfl", "torch"):
         os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "lora"
+        _native.refresh_env()
         try:
             x = x0.clone().requires_grad_(True)
             a = a0.clone().requires_grad_(True)
@@ -599,6 +606,7 @@ def test_lora_linear_fused_matches_unfused(T, with_res):
             res[route] = [y, x.grad, a.grad] + [b.grad for b in bs] + ([rr.grad] if with_res else [])
         finally:
             os.environ["BCFL_TORCH_OPS"] = ""
+            _native.refresh_env()
     for u, v in zip(res["bcfl"], res["torch"]):
         err = ((u.float() - v.float()).norm() / v.float().norm()).item()
         assert err < 1e-2, err
@@ -715,6 +723,7 @@ def test_lora_swiglu_mlp_matches_unfused(T):
     res = {}
     for route in ("bcfl", "torch"):
         os.environ["BCFL_TORCH_OPS"] = "" if route == "bcfl" else "lora"
+        _native.refresh_env()
         try:
             x, rr = x0.clone().requires_grad_(True), r0.clone().requires_grad_(True)
             agu, ad = agu0.clone().requires_grad_(True), ad0.clone().requires_grad_(True)
@@ -725,6 +734,7 @@ def test_lora_swiglu_mlp_matches_unfused(T):
             res[route] = [y, x.grad, rr.grad, agu.grad, ad.grad] + [b.grad for b in bgu + bd]
         finally:
             os.environ["BCFL_TORCH_OPS"] = ""
+            _native.refresh_env()
     for i, (u, v) in enumerate(zip(res["bcfl"], res["torch"])):
         err = ((u.float() - v.float()).norm() / v.float().norm()).item()
         assert err < 2e-2, (i, err)
