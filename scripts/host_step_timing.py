@@ -89,9 +89,15 @@ def main():
     wall = (time.perf_counter() - t0) / rounds
     dev = [a.elapsed_time(b) * 1e-3 for a, b in dev_steps]
     n = len(dev)
+    # device time from one step's end event to the next step's start event (the step boundary:
+    # AdamW has been issued before the end event; within a round only, steps 8 per round)
+    spr = n // max(rounds, 1)
+    gaps = [dev_steps[i][1].elapsed_time(dev_steps[i + 1][0]) * 1e-3
+            for i in range(n - 1) if (i + 1) % spr]
     out = {"rounds": rounds, "steps": n, "wall_s_per_round": wall,
            "host_issue_s_per_round": sum(rt) / rounds,
            "device_step_s_mean": sum(dev) / max(n, 1),
+           "device_step_boundary_gap_s_mean": sum(gaps) / max(len(gaps), 1),
            "host_step_parts_s_mean": {k: sum(v) / max(len(v), 1) for k, v in parts.items()},
            "note": "no profiler in these rounds; the cProfile below ran on 2 further rounds"}
     out["host_step_total_s_mean"] = sum(v for k, v in out["host_step_parts_s_mean"].items())

@@ -304,11 +304,13 @@ def _self_delay_worker(rank, world, out, kw):
 
 
 def test_mailbox_bounded_lead_holds_fast_rank_back(tmp_path):
-    """gossip_max_lead = 1: with one rank slowed by 400 ms per round the fast rank waits at round
+    """gossip_max_lead = 1: with one rank slowed by 1.2 s per round the fast rank waits at round
     starts (lead waits > 0) instead of running away, so the staleness it mixes stays within the
-    bound (+1 for the round in flight); unbounded it would drift several rounds ahead."""
+    bound (+1 for the round in flight); unbounded it would drift several rounds ahead. (The delay
+    must exceed a round's own time on a loaded CPU: at 400 ms the fast rank stayed under the
+    2-round lead that triggers a wait in one full-suite run.)"""
     res = run_world(_learn_worker, 2, str(tmp_path / "d"), str(tmp_path / "d"),
-                    {"inject_slow": {1: 400.0}, "liveness_timeout": 6, "gossip_max_lead": 1,
+                    {"inject_slow": {1: 1200.0}, "liveness_timeout": 6, "gossip_max_lead": 1,
                      "num_rounds": 8})
     assert float(res[0]["wait"]) > 0.0          # the fast rank was held back
     assert max(float(r["stale_max"]) for r in res) <= 3.0
