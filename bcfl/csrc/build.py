@@ -74,8 +74,19 @@ def _torch_flags():
 # instead of AGPRs — the attention kernels post-process every score tile with VALU ops, so AGPR
 # accumulators cost one v_accvgpr_read per element per tile; without them the flash-attention
 # kernels need no AGPRs at all and reach 3 waves/SIMD instead of 2.
+#
+# layernorm.hip is built WITHOUT packed-fp32 VALU ops (v_pk_mul / v_pk_add / v_pk_fma_f32). With
+# them, the LayerNorm backward kernel returned a different result for the last quarter of a wave
+# (lanes 48-63: one 128-byte group of one row, values a few bf16 ulps off) in ~10 % of the steps
+# when other client lanes ran concurrently — bitwise-identical inputs before and after the kernel,
+# and a re-run of the same kernel on those inputs reproducing the reference. Load type, cache
+# policy, acquire / release fences, the row pipeline, the cross-lane reduction and the block order
+# made no difference; the build without packed fp32 made 320 / 320 four-lane iterations bitwise
+# reproducible (scripts/kernel_determinism.py, profiles/lanes_determinism_r6.json). The kernels
+# are HBM-bound, so the scalar VALU form costs little.
 FILE_FLAGS = {
     "attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+    "layernorm.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
 }
 
 

@@ -360,9 +360,17 @@ class _BDALN(torch.autograd.Function):
     def backward(ctx, dout):
         z, mean, rstd, gamma = ctx.saved_tensors
         p8, ka, kb, has_b, has_r, has_beta = ctx.cfg
-        dy, dbias, dres, dgamma, dbeta = native().bdaln_bwd(dout.contiguous(), z, mean, rstd,
+        dout = dout.contiguous()
+        probe = _PROBE.get("bdaln")
+        if probe is not None:   # scripts/kernel_determinism.py DET_PROBE: inputs at kernel time
+            probe.append({"in": [t.clone() for t in (dout, z, mean, rstd, gamma)],
+                          "keys": (int(p8), int(ka), int(kb)), "has_b": bool(has_b)})
+        dy, dbias, dres, dgamma, dbeta = native().bdaln_bwd(dout, z, mean, rstd,
                                                             gamma, int(p8), int(ka), int(kb),
                                                             bool(has_b))
+        if probe is not None:
+            probe[-1]["out"] = [t.clone() for t in (dy, dres)]
+            probe[-1]["in_after"] = [t.clone() for t in (dout, z, mean, rstd, gamma)]
         if has_r and ctx.tap is not None:
             ctx.tap.g, dres = dres, None   # the consumer GEMM accumulates into it
         elif has_r and not p8 and _WG["enabled"]:
@@ -375,6 +383,10 @@ class _BDALN(torch.autograd.Function):
                 dbeta if has_beta else None, None, None, None, None, None)
 
 
+_RESIDUAL_TAP = os.environ.get("BCFL_RESIDUAL_TAP", "1") == "1"   # 0: autograd sums (A/B runs)
+_PROBE: dict = {}   # debugging hooks (scripts/kernel_determinism.py): op name -> record list
+
+
 def bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps: float, p: float = 0.0,
                                training: bool = False, tap: Optional[ResidualTap] = None):
     """LayerNorm(dropout(y + bias) + residual). ``tap`` (armed by the GEMM that also reads
@@ -384,7 +396,7 @@ def bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps: float, p: fl
     p8, ka, kb = _keys(p, training)
     if use_native(y, "bdaln"):
         use_tap = tap if (tap is not None and tap.armed and p8 and residual is not None
-                          and residual.requires_grad) else None
+                          and residual.requires_grad and _RESIDUAL_TAP) else None
         return _BDALN.apply(y.contiguous(), bias, residual, gamma, beta, eps, p8, ka, kb, use_tap)
     return ref.bias_dropout_add_layernorm(y, bias, residual, gamma, beta, eps, p8, ka, kb)
 

@@ -10,7 +10,9 @@ differ from the replica's first; the report names the parameters that differ, in
 
 DET_MODEL (default bert-base-2l) picks the model, DET_SERIAL=1 synchronises after every lane's
 step (the no-concurrency control), DET_SAVED=1 checks every saved activation between forward and
-backward; BCFL_TORCH_OPS / BCFL_G8_PERSIST bisect the kernels.
+backward, DET_TRACE=1 compares the gradients of the tensors around every LayerNorm, attention and
+FFN-down op, DET_PROBE=1 compares every LayerNorm backward's inputs and outputs at kernel time;
+BCFL_TORCH_OPS / BCFL_G8_PERSIST bisect the kernels.
 """
 import json
 import os
@@ -41,7 +43,8 @@ def main():
     for i in range(L):
         m = build_model(model_name, 2, device=dev, dtype=torch.bfloat16)
         flat = FlatParams.from_model(m, dev, torch.bfloat16)
-        rows = np.random.default_rng(100 + i).choice(len(ds), 32, replace=False)
+        same = os.environ.get("DET_SAME_BATCH") == "1"   # same shapes in every lane
+        rows = np.random.default_rng(100 + (0 if same else i)).choice(len(ds), 32, replace=False)
         b = pad_packed(make_packed_batch(ds, rows), 256).to(dev)
         lanes.append({"m": m, "flat": flat, "b": b, "s": torch.cuda.Stream(dev),
                       "rng": (1234 + 7 * i, 99 + i), "ref": None, "bad": 0})
@@ -50,6 +53,36 @@ def main():
     rng = ops.rng.global_rng()
     first_bad = []
     check_saved = os.environ.get("DET_SAVED") == "1"
+    # DET_PROBE=1: every LayerNorm backward's inputs and outputs, cloned right before / after the
+    # kernel on its stream, compared with the replica's first iteration
+    probe = os.environ.get("DET_PROBE") == "1"
+    from bcfl.ops import functional as F
+    trace = None
+    if os.environ.get("DET_TRACE") == "1":
+        # gradients of the intermediate tensors around every LayerNorm / attention / FFN-down op,
+        # cloned when autograd produces them: the first one (in backward order) that differs from
+        # the replica's first iteration names the op whose backward diverged
+        trace = {"cur": None}
+
+        def hooked(name, fn, argi):
+            def wrap(*a, **k):
+                out = fn(*a, **k)
+                rec = trace["cur"]
+                if rec is not None and torch.is_grad_enabled():
+                    o = out[0] if isinstance(out, tuple) else out
+                    tag = f"{name}#{rec['n']}"
+                    rec["n"] += 1
+                    if getattr(o, "requires_grad", False):
+                        o.register_hook(lambda g, tag=tag: rec["g"].append((tag + ".out", g.detach().clone())))
+                    for i in argi:
+                        t = a[i]
+                        if getattr(t, "requires_grad", False) and t.grad_fn is not None:
+                            t.register_hook(lambda g, tag=tag, i=i: rec["g"].append((f"{tag}.in{i}", g.detach().clone())))
+                return out
+            return wrap
+        ops.bias_dropout_add_layernorm = hooked("bdaln", ops.bias_dropout_add_layernorm, (0,))
+        ops.varlen_attention = hooked("attn", ops.varlen_attention, (0,))
+        ops.linear_after_act = hooked("ffn_down", ops.linear_after_act, (1,))
     for it in range(iters):
         for ln in lanes:
             with torch.cuda.stream(ln["s"]):
@@ -76,8 +109,15 @@ def main():
                         loss = ops.cross_entropy(ln["m"](ln["b"]), ln["b"].labels)
                     ln["marks"] = marks
                 else:
+                    if trace is not None:
+                        trace["cur"] = ln["tr"] = {"n": 0, "g": []}
                     loss = ops.cross_entropy(ln["m"](ln["b"]), ln["b"].labels)
+                    if trace is not None:
+                        trace["cur"] = None
+                if probe:
+                    F._PROBE["bdaln"] = ln["probe"] = []
                 backward(loss)
+                F._PROBE.pop("bdaln", None)
                 ops.join_wgrad(dev)
                 g = torch.cat([p.grad.reshape(-1).float() for p in ln["flat"].params])
                 ln["out"] = (loss.detach().float().clone(), g)
@@ -91,6 +131,60 @@ def main():
                     print(json.dumps({"iter": it, "lane": k, "saved_tensor_changed": i,
                                       "shape": shp, "dtype": dt, "elements": int(n)}), flush=True)
             loss, g = ln["out"]
+            if probe:
+                if ln["ref"] is None:
+                    ln["ref_probe"] = ln["probe"]
+                else:
+                    for j, (a, b) in enumerate(zip(ln["probe"], ln["ref_probe"])):
+                        din = [int((x != y).sum()) for x, y in zip(a["in"], b["in"])]
+                        din_after = [int((x != y).sum()) for x, y in zip(a["in_after"], a["in"])]
+                        dout_ = [int((x != y).sum()) for x, y in zip(a["out"], b["out"])]
+                        if any(din) or any(dout_) or a["keys"] != b["keys"]:
+                            rows = torch.nonzero((a["out"][0] != b["out"][0]).any(1)).flatten()
+                            # the same kernel re-run now, on the inputs cloned right before the
+                            # original launch: does it reproduce the reference outputs?
+                            x = a["in"]
+                            rr = F.native().bdaln_bwd(x[0], x[1], x[2], x[3], x[4], *a["keys"], a["has_b"])
+                            torch.cuda.synchronize()
+                            rerun_vs_ref = [int((rr[0] != b["out"][0]).sum()), int((rr[2] != b["out"][1]).sum())]
+                            rerun_vs_orig = [int((rr[0] != a["out"][0]).sum()), int((rr[2] != a["out"][1]).sum())]
+                            # the 16-element groups that differ: (row, first column)
+                            dif = (a["out"][0] != b["out"][0])
+                            cols = [(int(r_), int(torch.nonzero(dif[r_]).flatten()[0]), int(torch.nonzero(dif[r_]).flatten()[-1]))
+                                    for r_ in rows[:4].tolist()]
+                            # sample values: this run, the reference, and the other lanes' outputs
+                            # of the same call at the same position (cross-lane contamination?)
+                            r0 = int(rows[0])
+                            c0 = torch.nonzero(dif[r0]).flatten()[:4].tolist()
+                            samp = {"got": [float(a["out"][1][r0, c]) for c in c0],
+                                    "ref": [float(b["out"][1][r0, c]) for c in c0],
+                                    "dout": [float(a["in"][0][r0, c]) for c in c0]}
+                            for k2, ln2 in enumerate(lanes):
+                                pr2 = ln2.get("probe") if k2 != k else None
+                                if pr2 and j < len(pr2) and pr2[j]["out"][1].shape == a["out"][1].shape:
+                                    samp[f"lane{k2}"] = [float(pr2[j]["out"][1][r0, c]) for c in c0]
+                            print(json.dumps({"iter": it, "lane": k, "ln_bwd_call": j,
+                                              "inputs_differing": din, "outputs_differing": dout_,
+                                              "inputs_changed_during_kernel": din_after,
+                                              "keys_equal": a["keys"] == b["keys"],
+                                              "dy_rows": rows[:8].tolist(),
+                                              "rerun_vs_ref": rerun_vs_ref, "rerun_vs_orig": rerun_vs_orig,
+                                              "row_first_last_col": cols, "samples": samp}), flush=True)
+                            break
+            if trace is not None:
+                if ln["ref"] is None:
+                    ln["ref_tr"] = ln["tr"]["g"]
+                else:
+                    for (tag, a), (_, b) in zip(ln["tr"]["g"], ln["ref_tr"]):
+                        if not torch.equal(a, b):
+                            nd = int((a != b).sum())
+                            rows = torch.nonzero((a != b).reshape(a.shape[0], -1).any(1)).flatten()
+                            print(json.dumps({"iter": it, "lane": k, "first_grad_diff": tag,
+                                              "shape": list(a.shape), "elements": nd,
+                                              "rows": rows[:12].tolist(), "nrows": int(rows.numel()),
+                                              "max_abs": float((a.float() - b.float()).abs().max())}),
+                                  flush=True)
+                            break
             if ln["ref"] is None:
                 ln["ref"] = (loss, g)
                 continue
