@@ -1,0 +1,14 @@
+# Round 6 final measurements: GPU suite, smoke(), the N = 1 driver bench (20 timed + 5 warm-up),
+# the one-client layout, rocprofv3 kernel stats of both, and two worker-grid reps.
+set -o pipefail
+O=${1:-gpurun_out/r6final}
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 180 --timeout-method thread tests > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench8.json 2> $O/bench8.err || exit 1
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --clients 1 --global-test-samples 125 > $O/bench1.json 2> $O/bench1.err || exit 1
+bash scripts/profile_bench.sh r6f1 --clients 1 --global-test-samples 125 > $O/prof1.log 2>&1 || exit 1
+bash scripts/profile_bench.sh r6f8 > $O/prof8.log 2>&1 || exit 1
+timeout -k 10 900 python -u benchmarks/worker_grid.py --clients 5 10 20 --rounds 20 --out $O/grid_rep1.json > $O/grid_rep1.log 2>&1 || exit 1
+timeout -k 10 900 python -u benchmarks/worker_grid.py --clients 5 10 20 --rounds 20 --out $O/grid_rep2.json > $O/grid_rep2.log 2>&1 || exit 1
