@@ -190,6 +190,11 @@ class FLConfig:
     anomaly_k: float = 2.0              # reject below mean - k*std of PageRank
     anomaly_modz_threshold: float = 3.5
     sketch_dim: int = 8192
+    filter_redistribute: str = "similar"  # asynchronous filter: a rejected source's mixing share goes
+                                        # to the accepted sources its first rejected update pointed
+                                        # like (sketch cosine > 0: on label shards its class-mates) |
+                                        # "uniform" (8 label-shard clients, one Byzantine: 0.98 vs
+                                        # never leaving the majority rate, tests/test_loopback.py)
     ledger: bool = True
     topology_probe: bool = False        # measure xGMI bandwidth matrix and filter peers by PageRank
     # --- fault injection -----------------------------------------------------------
@@ -256,6 +261,7 @@ class FLConfig:
                    "gossip_self_delay": ("off", "on"),
                    "lr_schedule": ("constant", "linear", "cosine"),
                    "anomaly_filter": ("none", "pagerank", "modz", "both"),
+                   "filter_redistribute": ("similar", "uniform"),
                    "fedavg_weighting": ("examples", "batches", "uniform"),
                    "global_eval_models": ("all", "client0", "average")}
         for k, allowed in choices.items():

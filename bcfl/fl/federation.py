@@ -303,7 +303,7 @@ class Federation(LanesMixin, EvalMixin, TrustMixin, ServerRoundMixin,
                         and self.gossip.apply_mode == "complete"):
                     # asynchronous trust: every complete round is judged by each receiver before
                     # it is applied (no collective, no previous-round verdicts)
-                    self.gossip.enable_filter(self.filter, cfg.sketch_dim)
+                    self.gossip.enable_filter(self.filter, cfg.sketch_dim, cfg.filter_redistribute)
                     self._gossip_filter = True
                     self.collective_free = True
                 if (self.gossip.apply_mode == "complete" and self.drift.exchange

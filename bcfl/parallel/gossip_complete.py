@@ -15,7 +15,7 @@ from .gossip import _nullctx
 
 
 class CompleteApplyMixin:
-    def enable_filter(self, filt, sketch_dim: int = 8192) -> None:
+    def enable_filter(self, filt, sketch_dim: int = 8192, redistribute: str = "similar") -> None:
         """Asynchronous update anomaly filtering (round-complete delta exchange): when round T is
         complete, the receiver measures every source's round-T update ``S_j^T - S_j^applied`` (a
         signed block sketch and its norm, one fused pass, ops.update_stats), runs ``filt``
@@ -27,6 +27,8 @@ class CompleteApplyMixin:
             raise ValueError("in-gossip anomaly filtering needs the round-complete delta exchange")
         self.filter = filt
         self.sketch_dim = int(sketch_dim)
+        self.redistribute = redistribute
+        self._redis = {}
 
     def take_verdicts(self) -> List[tuple]:
         """(round, rejected sources) of every application since the last call."""
@@ -48,6 +50,23 @@ class CompleteApplyMixin:
         a = torch.stack(rows).cpu().double().numpy()
         v = self.filter(a[:, :-1], a[:, -1])
         rej = {js[i] for i in v.rejected}
+        # where a rejected source's share goes (_row): to the accepted sources its FIRST rejected
+        # update pointed like (sketch cosine, clamped at 0) — on label shards its class-mates, so
+        # the accepted updates stay class-balanced (re-normalising uniformly left 3 vs 4 clients
+        # per class and a federation stuck at the majority rate); uniformly when nothing points
+        # its way. The map is kept: later updates of a rejected client carry the drift
+        # correction towards the other classes and no longer point at its class-mates. An
+        # attacker can only move its own share among honest clients.
+        if rej and self.redistribute == "similar":
+            sk = a[:, :-1]
+            nrm = np.linalg.norm(sk, axis=1)
+            nrm[nrm == 0] = 1.0
+            u = sk / nrm[:, None]
+            for i in v.rejected:
+                if js[i] in self._redis:
+                    continue   # the map of the first round a source was rejected in is kept
+                self._redis[js[i]] = {js[k]: max(0.0, float(u[i] @ u[k]))
+                                      for k in range(len(js)) if js[k] not in rej}
         for i, j in enumerate(js):
             self.records.append({"client": j, "kind": "verdict", "round": int(T),
                                  "ok": j not in rej, "reason": v.reasons.get(i, ""),
@@ -68,6 +87,15 @@ class CompleteApplyMixin:
         W = self.W_mid
         full = sum(float(W[c, j]) for j in self.sources)
         ws = [0.0 if j in rej else float(W[c, j]) for j in js]
+        red = getattr(self, "_redis", {})
+        for r in rej:
+            sims = red.get(r)
+            share = float(W[c, r])
+            if share > 0 and sims:
+                tot = sum(sims.get(j, 0.0) for j in js if j not in rej)
+                if tot > 0:
+                    ws = [w + (share * sims.get(j, 0.0) / tot if j not in rej else 0.0)
+                          for w, j in zip(ws, js)]
         keep = sum(ws)
         f = full / keep if keep > 0 else 0.0
         a = (self.apply_scale if scaled else 1.0) * f

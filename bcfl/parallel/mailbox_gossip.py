@@ -645,7 +645,9 @@ class MailboxGossip(CompleteApplyMixin):
                 "rejected_version": {int(k): int(v) for k, v in self.rejected_version.items()},
                 "seen_round": {int(k): int(v) for k, v in self.seen_round.items()},
                 "slot_meta": {int(c): [list(x) for x in m] for c, m in self.slot_meta.items()},
-                "records": _portable_records(self.records)}
+                "records": _portable_records(self.records),
+                "redistribute": {int(r): {int(j): float(w) for j, w in m.items()}
+                                 for r, m in getattr(self, "_redis", {}).items()}}
 
     def load_state_dict(self, st: dict):
         for c, bufs in st["send_buf"].items():
@@ -670,3 +672,6 @@ class MailboxGossip(CompleteApplyMixin):
         self.seen_round.update({int(k): int(v) for k, v in st.get("seen_round", {}).items()})
         for c, m in st.get("slot_meta", {}).items():
             self.slot_meta[int(c)] = [tuple(int(y) for y in x) for x in m]
+        if st.get("redistribute"):
+            self._redis = {int(r): {int(j): float(w) for j, w in m.items()}
+                           for r, m in st["redistribute"].items()}
