@@ -14,7 +14,8 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 pr = d.get("multi_rank", {}).get("per_rank", [])
 print(sys.argv[2], "s/round", round(d["value"], 4), "final", d["final_accuracy"], "curve", d["accuracy_curve"])
-print("  stale mean", [round(sum(p["stale_rounds"]) / max(1, len(p["stale_rounds"])), 2) for p in pr],
-      "wait s", [round(p["wait_s_total"], 2) for p in pr], "lead wait s",
-      [round(p.get("lead_wait_s_total", 0), 2) for p in pr])
+st = lambda p: [x for x in (p.get("stale_rounds") or []) if x is not None]  # noqa: E731
+print("  stale mean", [round(sum(st(p)) / max(1, len(st(p))), 2) for p in pr],
+      "wait s", [round(p.get("wait_s_total") or 0.0, 2) for p in pr], "lead wait s",
+      [round(p.get("lead_wait_s_total") or 0.0, 2) for p in pr])
 PY
