@@ -1113,6 +1113,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bias", &wgrad_bias);
   m.def("gemm8", &gemm8);
   m.def("set_wgrad_kernel", &set_wgrad_kernel);
+  m.def("set_wgrad_slots", &bcfl::set_wgrad_slots, "weight-gradient tile slots (0 = 64)");
   m.def("set_g8_block_rows", &bcfl::set_g8_block_rows,
         "pin the block rows (128 / 256) of auto-tiled 8-phase GEMM launches; 0 = auto");
   m.def("set_g8_persistent", &bcfl::set_g8_persistent,

@@ -759,8 +759,10 @@ int g8_dispatch(const G8Params& p, hipStream_t s) {
 
 }  // namespace
 
+extern int g8_wgrad_slots_pinned;
 void set_g8_persistent(bool on) { g8_persist_default = on; }
 void set_g8_block_rows(int bm) { g8_bm_pinned = (bm == 128 || bm == 256) ? bm : 0; }
+void set_wgrad_slots(int slots) { g8_wgrad_slots_pinned = slots > 0 ? slots : 0; }
 
 // Weight gradient dW[N, K] = G[M, N]^T X[M, K] on the 8-phase kernel: A = G (transposed reads),
 // B = X (transposed reads), reduction over the M tokens split into S slices so the grid covers
@@ -769,14 +771,21 @@ void set_g8_block_rows(int bm) { g8_bm_pinned = (bm == 128 || bm == 256) ? bm : 
 // mean less fp32 partial traffic); fp32 slice partials are summed by
 // the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials the
 // n-tile-0 workgroups produce in the main loop (G^T . ones on MFMA: no second pass over G).
+// tile slots pinned by the runtime (0 = 64): a rank that trains ONE client lane uses 96 — with the
+// caller-thread backward the one-client step's device time drops 2.2 % against 64 (3 interleaved
+// reps, profiles/host_issue_r6.json); with concurrent lanes the chip is full and 64 stays
+int g8_wgrad_slots_pinned = 0;
+
 int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override) {
   if (N % BN8 || K % BN8 || N <= 0 || M <= 0) return 0;
   static const int slots_env = [] {
     const char* e = std::getenv("BCFL_G8_WGRAD_SLOTS");
-    const int v = e ? std::atoi(e) : 64;  // 1-client round: 64 slots 0.0927 s, 128 0.0942, 256 0.0968
-    return v > 0 ? v : 64;
+    const int v = e ? std::atoi(e) : 0;  // round 5, 1-client round: 64 slots 0.0927 s, 128 0.0942, 256 0.0968
+    return v > 0 ? v : 0;
   }();
-  const int slots = slots_override > 0 ? slots_override : slots_env;
+  const int slots = slots_override > 0 ? slots_override
+                    : slots_env > 0 ? slots_env
+                    : g8_wgrad_slots_pinned > 0 ? g8_wgrad_slots_pinned : 64;
   const int tiles = (N / BN8) * (K / BN8);  // 256 x 256 output tiles of dW[N, K]
   int S = (slots + tiles - 1) / tiles;
   const int maxS = M / 1024 > 0 ? M / 1024 : 1;  // keep >= 16 K-tiles per slice

@@ -112,6 +112,7 @@ int wgrad_g8_bias_parts(int S);  // rows of the bias-partial buffer the g8 weigh
 int wgrad_g8_splits(int M, int N, int K, int* Mc, int slots_override = 0);  // slots: 0 = default
 void set_g8_block_rows(int bm);   // 128 / 256 pins the block rows of auto-tiled g8 launches, 0 = auto
 void set_g8_persistent(bool on);  // persistent BM=128 g8 grids (BCFL_G8_PERSIST overrides)
+void set_wgrad_slots(int slots);  // weight-gradient tile slots, 0 = 64 (BCFL_G8_WGRAD_SLOTS overrides)
 int launch_wgrad_g8(const WgradParams& p, hipStream_t s);
 
 // ---- skinny.hip: tall-skinny LoRA products (HBM-bound) ---------------------------------------
