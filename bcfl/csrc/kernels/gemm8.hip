@@ -772,7 +772,7 @@ void set_wgrad_slots(int slots) { g8_wgrad_slots_pinned = slots > 0 ? slots : 0;
 // the deterministic reduce kernel (gemm.hip), which also sums the bias-gradient partials the
 // n-tile-0 workgroups produce in the main loop (G^T . ones on MFMA: no second pass over G).
 // tile slots pinned by the runtime (0 = 64): a rank that trains ONE client lane uses 96 — with the
-// caller-thread backward the one-client step's device time drops 2.2 % against 64 (3 interleaved
+// caller-thread backward the one-client round drops 2.9 % against 64 (3 interleaved
 // reps, profiles/host_issue_r6.json); with concurrent lanes the chip is full and 64 stays
 int g8_wgrad_slots_pinned = 0;
 

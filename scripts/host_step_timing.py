@@ -116,6 +116,11 @@ def main():
     s = io.StringIO()
     pstats.Stats(prof, stream=s).sort_stats("cumtime").print_stats(60)
     print(s.getvalue())
+    # who blocks the host on the device (host reads / synchronisations) per round
+    s = io.StringIO()
+    st = pstats.Stats(prof, stream=s)
+    st.print_callers("method 'cpu'|synchronize|method 'item'|method 'tolist'")
+    print(s.getvalue())
 
 
 if __name__ == "__main__":
