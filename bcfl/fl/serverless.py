@@ -213,7 +213,12 @@ class ServerlessRoundMixin:
                         self._launch_eval_local(c, r)
                     else:
                         local_eval[c] = self.trainer.evaluate_device(self.test_batches(c, r))
-            root = self._merkle() if self.ledger is not None and not self._gossip_roots else ""
+            root = ""
+            if self.ledger is not None and not self._gossip_roots:
+                # the deferred ledger (below) reads a device root when the round's tail is done;
+                # a host read here would drain the GPU in front of the round's remaining launches
+                root = (ops.merkle_root_deferred(self.flat.master) if self._host_deferred
+                        else self._merkle())
             recs.append({"client": c, "root": root, "ts": float(r) + 0.001 * (c + 1),
                          "verdict": "accept", "metrics": {"examples": st["examples"]}})
             self._deactivate(c)
@@ -263,7 +268,7 @@ class ServerlessRoundMixin:
                 self._launch_eval_global(r)   # filed under round r by _resolve_eval
             else:
                 ge = self._eval_global(r)
-        host_deferred = self.collective_free and self.is_cuda and not self.rt.distributed
+        host_deferred = self._host_deferred
         client_metrics = []
         if host_deferred and local_eval:
             # the lanes' local scores are read at the next round's start with the other deferred
@@ -275,7 +280,7 @@ class ServerlessRoundMixin:
         ledger_extra = {"kind": "mix", "rejected": sorted(v.rejected),
                         "stale_rounds": info.get("stale_rounds", 0.0),
                         "dead_peers": sorted(self.gossip.dead)}
-        if self.collective_free and self.is_cuda and not self.rt.distributed:
+        if host_deferred:
             # nothing of this round is read back on the host now (the loss sum and the ledger's
             # Merkle roots wait for the round's last kernels): the next round's work is queued
             # while this round's tail still runs, and the reads happen at its start. Multi-rank
@@ -304,6 +309,12 @@ class ServerlessRoundMixin:
                    if self._gossip_filter else {})}
 
     # ---- host reads deferred to the next round --------------------------------------------------
+    @property
+    def _host_deferred(self) -> bool:
+        """One-process collective-free GPU runs read a round's results at the next round start."""
+        return (self.collective_free and self.is_cuda and not self.rt.distributed
+                and not os.environ.get("BCFL_ROUND_SYNC"))
+
     def _defer(self, fn) -> None:
         """Queue a host read of this round's device results. It runs once the work queued so far
         has finished on the device (an event recorded now), so a read never stalls the host in
