@@ -101,6 +101,9 @@ def check_wgrad(dev):
     return res
 
 
+TR = False
+
+
 def bench_wgrad(dev, reps):
     import os
     C = native()
@@ -120,6 +123,26 @@ def bench_wgrad(dev, reps):
             os.environ["BCFL_WGRAD_G8"] = "1"
             return C.wgrad_bias(G, X)
         arms = {"hipblaslt": lambda: (G.t() @ X, G.sum(0)), "k9": k9, "g8": g8}
+        if TR:   # the weight gradient as a forward-layout GEMM over transposed operands
+            GT, XT = G.t().contiguous(), X.t().contiguous()
+
+            def tr_gemm(gt, xt, bm, S):
+                if S == 1:
+                    return C.gemm8(gt, xt, False, False, 0, 0, None, None, None, bm, 1, 0)[0]
+                kc = (M // S + 63) // 64 * 64
+                return C.gemm8(gt, xt, False, False, 5, 0, None, None, None, bm,
+                               -(-M // kc), kc)[0].sum(0)
+            arms = {"g8_nobias": lambda: C.wgrad(G, X, 0),
+                    "transpose_only": lambda: (G.t().contiguous(), X.t().contiguous()),
+                    **{f"pre_tr_bm{bm}_s{S}": (lambda bm=bm, S=S: tr_gemm(GT, XT, bm, S))
+                       for bm in (128, 256) for S in (1, 2, 4)},
+                    "tr_bm128_s2": lambda: tr_gemm(G.t().contiguous(), X.t().contiguous(), 128, 2)}
+            ref = G.float().t() @ X.float()
+            for k, f in arms.items():
+                if k.startswith(("pre_tr", "tr_")):
+                    o = f().float()
+                    rel = ((o - ref).norm() / ref.norm()).item()
+                    assert rel < 1e-2, (k, rel)
         for f in arms.values():
             f()
         torch.cuda.synchronize()
@@ -205,10 +228,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--wgrad-only", action="store_true")
+    ap.add_argument("--wgrad-transposed", action="store_true",
+                    help="time the weight gradient as a forward-layout GEMM on transposed operands")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default="gpurun_out/g8.json")
     a = ap.parse_args()
     dev = torch.device("cuda")
+    global TR
+    TR = a.wgrad_transposed
     t0 = time.time()
     res = {"check": check(dev), "check_wgrad": check_wgrad(dev)}
     ok = all(r["ok"] and r["epi_ok"] for r in res["check"]) and all(r["ok"] for r in res["check_wgrad"])
