@@ -177,6 +177,10 @@ class FLConfig:
     #                                     measured slower on BERT-base, so off by default)
     overlap_wgrad: Optional[bool] = None  # weight-gradient GEMMs on a side stream (GPU);
                                           # None = auto: on when a rank trains one client at a time
+    wgrad_slots: int = 0                # split-K tile slots of the weight-gradient GEMM; 0 = auto
+                                        # (96 on a one-lane rank, 64 with lanes). The split count sets
+                                        # the fp32 summation order, so runs with different lane counts
+                                        # are bitwise equal only with the same explicit value
     micro_batches: int = 0              # a rank training ONE client at a time splits each batch into
                                         # 2 micro-batches trained concurrently on 2 streams (second
                                         # replica sharing the weights, gradients summed in AdamW);
@@ -267,6 +271,8 @@ class FLConfig:
         for k, allowed in choices.items():
             if getattr(self, k) not in allowed:
                 raise ValueError(f"{k}={getattr(self, k)!r}: expected one of {allowed}")
+        if self.wgrad_slots < 0:
+            raise ValueError(f"wgrad_slots={self.wgrad_slots}: expected 0 (auto) or a slot count")
         if self.mode == "server" and self.server_transport != "rccl" and self.anomaly_filter != "none":
             raise ValueError("server_transport='mailbox' aggregates without collectives; the update "
                              "anomaly filter needs the global view (use server_transport='rccl')")

@@ -168,7 +168,7 @@ class Federation(LanesMixin, EvalMixin, TrustMixin, ServerRoundMixin,
             big = self.flat.numel > 1_000_000_000
             ops.native().set_g8_block_rows(256 if len(self.lanes) > 1 and not big else 0)
             # one lane: the side-stream weight gradient may take 96 tile slots (64 with lanes)
-            ops.native().set_wgrad_slots(96 if len(self.lanes) <= 1 else 0)
+            ops.native().set_wgrad_slots(cfg.wgrad_slots or (96 if len(self.lanes) <= 1 else 64))
         self.global_master: Optional[torch.Tensor] = None
         if cfg.mode == "server":
             self.global_master = self.flat.master.detach().clone()

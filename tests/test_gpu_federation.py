@@ -24,7 +24,7 @@ def _run(tmp, lanes, overlap, **kw):
                    train_samples=64, test_samples=32, global_test_samples=64,
                    out_dir=tmp, reference_prints=False, client_lanes=lanes, overlap_wgrad=overlap,
                    async_gossip=False, gossip_transport="rccl", ledger=True, save_every=0,
-                   dropout=0.1, drift_correction="scaffold", **kw)
+                   dropout=0.1, drift_correction="scaffold", wgrad_slots=64, **kw)
     fed = Federation(cfg, verbose=False)
     assert len(fed.lanes) == lanes
     h = fed.run()
@@ -40,7 +40,8 @@ def test_gpu_lanes_match_sequential(tmp_path, lanes, overlap):
     """Every BERT GEMM (the 8-phase gemm8 kernels, including the weight gradients), the
     attention and the reductions are bcfl's own deterministic kernels, so concurrent lanes and
     side-stream weight gradients reproduce one-lane training BIT FOR BIT: masters, loss curve
-    and the ledger's update roots. (The K9 weight-gradient kernel of gemm.hip only serves shapes
+    and the ledger's update roots, at the same weight-gradient split count (``wgrad_slots``; the
+    auto value differs between one lane and several). (The K9 weight-gradient kernel of gemm.hip only serves shapes
     that are not 256-multiples — ALBERT's 128-wide embedding projection — and is pinned by
     tests/test_gpu_kernels.py::test_wgrad_split_m.)"""
     a = _run(str(tmp_path / "ref"), 1, False)
