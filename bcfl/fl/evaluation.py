@@ -4,6 +4,7 @@ overlapped evaluation, deferred local scores and the server's hold-out gate (mix
 ``test()`` (``src/Serverlesscase/serverless_IID_IMDB.py:172-187,235-246``, ``src/Servercase/server_IID_IMDB.py:121-135``)."""
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -20,6 +21,23 @@ from ..parallel.gossip import MailboxGossip
 from .trainer import EvalResult, LocalTrainer
 from .fedutil import weighted_average
 from .lanes import _share_frozen
+
+
+# BCFL_EVAL_READ_SYNC=1: read evaluation results with .cpu() at resolve time (A/B baseline)
+_SYNC_READS = bool(os.environ.get("BCFL_EVAL_READ_SYNC"))
+# BCFL_EVAL_LOCAL_EARLY=1: issue a local evaluation right after its snapshot (A/B baseline)
+_EARLY_LOCAL = bool(os.environ.get("BCFL_EVAL_LOCAL_EARLY"))
+
+
+def _host_copy(t: torch.Tensor) -> torch.Tensor:
+    """Queue a D2H copy of a small device result on the CURRENT stream into pinned host memory
+    (record the completion event after it). ``t.cpu()`` at read time would synchronise the reading
+    thread's current stream — the training stream — and drain every launch queued on it."""
+    if _SYNC_READS:
+        return t
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    return h
 
 
 class EvalMixin:
@@ -227,36 +245,66 @@ class EvalMixin:
             sets = self._global_eval_sets(r)   # first use uploads on the current stream
             main = torch.cuda.current_stream(self.device)
             es = self.eval_stream
-            es.wait_stream(main)               # the mixed model(s) and the batches are ready
             if not hasattr(self, "_eval_snaps"):
                 self._eval_snaps = {}
+            # the snapshots are taken on the TRAINING stream: later writers of the sources (next
+            # round's optimizer / mixing) are ordered after them by stream order, and the training
+            # stream never waits for the side stream (a copy queued there would wait behind the
+            # local evaluation already running on it). The previous global evaluation, the only
+            # reader of these buffers, was resolved (synchronised) above.
+            snaps = []
+            for c, _ in sets:
+                if len(sets) == 1:
+                    snap = self.eval_flat.param
+                else:
+                    snap = self._eval_snaps.get(c)
+                    if snap is None:
+                        snap = self._eval_snaps[c] = torch.empty_like(self.eval_flat.param)
+                snap.copy_(self._client_param(c))
+                snaps.append(snap)
+            es.wait_stream(main)               # the snapshots and the batches are ready
             with torch.cuda.stream(es):
                 t_beg = torch.cuda.Event(enable_timing=True)
                 t_beg.record(es)
-                snaps = []
-                for c, _ in sets:
-                    if len(sets) == 1:
-                        snap = self.eval_flat.param
-                    else:
-                        snap = self._eval_snaps.get(c)
-                        if snap is None:
-                            snap = self._eval_snaps[c] = torch.empty_like(self.eval_flat.param)
-                    snap.copy_(self._client_param(c))
-                    snaps.append(snap)
-                copied = torch.cuda.Event()
-                copied.record(es)
-                # later writers of the sources (next round's optimizer / mixing, issued on main
-                # or on lane streams that wait on main) are ordered after the snapshot copies
-                # only; the forward passes overlap them
-                main.wait_event(copied)
                 acc = torch.zeros(4, dtype=torch.float64, device=self.device)
                 for (c, gb), snap in zip(sets, snaps):
                     if gb:
                         self.eval_flat.rebind(self.eval_flat.master, snap)
-                        acc += self.eval_trainer.evaluate_device(gb)
+                        acc += self._eval_forward(snap, gb)
+                # collective-free: the counts cross to pinned host memory on the side stream, so
+                # the host read never synchronises the training stream (acc.cpu() would: it drains
+                # the round queued on the reading thread's current stream first)
+                self._eval_host = _host_copy(acc) if self.collective_free and not _SYNC_READS else None
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(es)
             self._eval_pending = (r, acc, sets, ev, t_beg)
+
+    def _eval_forward(self, snap: torch.Tensor, batches) -> torch.Tensor:
+        """The side stream's evaluation of the replica bound to ``snap`` on ``batches`` (cached,
+        fixed device batches): eager the first time, then captured once into a hipGraph per
+        (snapshot buffer, batch set) and replayed. A BERT-base forward over a few batches is ~200
+        launches, ~2.2 ms of host issue per evaluation, which with one client per GPU the host
+        spent while the training stream had nothing queued; a replay is one launch. The graph
+        reads the same snapshot buffer and batches every round (both kept alive with it) and
+        runs exactly the eager kernels. ``BCFL_EVAL_GRAPHS=0`` keeps the eager issue."""
+        if os.environ.get("BCFL_EVAL_GRAPHS", "1") == "0" or not batches:
+            return self.eval_trainer.evaluate_device(batches)
+        if not hasattr(self, "_eval_graphs"):
+            self._eval_graphs, self._eval_seen = {}, set()
+        key = (snap.data_ptr(), id(batches))
+        ent = self._eval_graphs.get(key)
+        if ent is None:
+            if key not in self._eval_seen:   # first use eager: allocator and kernels warm
+                self._eval_seen.add(key)
+                return self.eval_trainer.evaluate_device(batches)
+            g = torch.cuda.CUDAGraph()
+            # thread-local capture: the checkpoint writer thread may copy concurrently
+            with torch.cuda.graph(g, stream=torch.cuda.current_stream(self.device),
+                                  capture_error_mode="thread_local"):
+                out = self.eval_trainer.evaluate_device(batches)
+            ent = self._eval_graphs[key] = (g, out, batches, snap)
+        ent[0].replay()
+        return ent[1]
 
     def _resolve_eval(self) -> None:
         """Host-read a queued global evaluation and file it under its round."""
@@ -264,11 +312,12 @@ class EvalMixin:
         if p is None:
             return
         r, acc, _sets, ev, t_beg = p
+        host, self._eval_host = getattr(self, "_eval_host", None), None
         ev.synchronize()
         self.timer.add_hidden("eval_global", t_beg.elapsed_time(ev) / 1000.0)
         if not self.collective_free:
             D.all_reduce_(acc)
-        a = acc.cpu().tolist()
+        a = host.tolist() if host is not None else acc.cpu().tolist()
         ge = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
         self._note_global_counts(r, a)
         self.global_accuracies.append(ge.accuracy)
@@ -347,44 +396,73 @@ class EvalMixin:
                 and not self.rt.distributed)
 
     def _launch_eval_local(self, c: int, r: int) -> None:
+        """Snapshot client c's trained model on the training stream; its forward passes are
+        issued on the side stream by :meth:`_issue_eval_local` after the round's exchange, so the
+        host queues the round-end work of the training stream (commitment, exchange, mixing)
+        first: with one client per GPU the host is barely ahead of the device at the end of
+        training, and issuing ~200 evaluation kernels there left the training stream idle."""
         main = torch.cuda.current_stream(self.device)
         if not hasattr(self, "_local_snaps"):
             self._local_snaps = [torch.empty_like(self.flat.param) for _ in range(2)]
             self._local_done: List[Optional[torch.cuda.Event]] = [None, None]
             self._local_pending: List[tuple] = []
+            self._local_queued: List[tuple] = []
             self._local_k = 0
         i = self._local_k % 2
         self._local_k += 1
+        if any(q[5] == i for q in self._local_queued):
+            self._issue_eval_local()               # its snapshot slot is about to be reused
         if self._local_done[i] is not None:
             main.wait_event(self._local_done[i])   # the evaluation that last read this snapshot
         snap = self._local_snaps[i]
         snap.copy_(self.flat.param)                # the trained model, before the mix
         batches = self.test_batches(c, r)          # uploaded on the training stream
-        es = self.eval_stream
-        es.wait_stream(main)
-        own = self.eval_flat.param
-        with torch.cuda.stream(es):
-            self.eval_flat.rebind(self.eval_flat.master, snap)
-            stats = self.eval_trainer.evaluate_device(batches)
-            ev = torch.cuda.Event()
-            ev.record(es)
-        # the queued kernels hold the snapshot's pointers; the replica's own buffer is what the
-        # global evaluation copies into (no later reader of the snapshot but this evaluation)
-        self.eval_flat.rebind(self.eval_flat.master, own)
-        self._local_done[i] = ev
-        # the batches stay referenced until the statistics are read (their memory belongs to
-        # the training stream's pool)
-        self._local_pending.append((r, c, stats, ev, batches))
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self._local_queued.append((r, c, snap, batches, ready, i))
+        if _EARLY_LOCAL:
+            self._issue_eval_local()
 
-    def _resolve_eval_local(self) -> None:
+    def _issue_eval_local(self) -> None:
+        """Queue the forward passes of the snapshotted local evaluations on the side stream."""
+        q = getattr(self, "_local_queued", None)
+        if not q:
+            return
+        self._local_queued = []
+        es = self.eval_stream
+        own = self.eval_flat.param
+        for r, c, snap, batches, ready, i in q:
+            es.wait_event(ready)
+            with torch.cuda.stream(es):
+                self.eval_flat.rebind(self.eval_flat.master, snap)
+                stats = self._eval_forward(snap, batches)
+                host = _host_copy(stats)
+                ev = torch.cuda.Event()
+                ev.record(es)
+            self._local_done[i] = ev
+            # the batches stay referenced until the statistics are read (their memory belongs to
+            # the training stream's pool)
+            self._local_pending.append((r, c, host, ev, batches))
+        # the queued kernels hold the snapshots' pointers; the replica's own buffer is what the
+        # global evaluation copies into (no later reader of a snapshot but its evaluation)
+        self.eval_flat.rebind(self.eval_flat.master, own)
+
+    def _resolve_eval_local(self, block: bool = True) -> None:
+        """File the deferred local scores. ``block=False`` (the round start) files only those
+        whose evaluation has finished: the last round's is usually still running on the side
+        stream, and waiting for it there left the training stream idle ~5 ms per round."""
+        self._issue_eval_local()
         pend = getattr(self, "_local_pending", None)
         if not pend:
             return
-        self._local_pending = []
+        k = 0
+        while k < len(pend) and (block or pend[k][3].query()):
+            k += 1
+        pend, self._local_pending = pend[:k], pend[k:]
         by_round: Dict[int, list] = {}
-        for r, c, stats, ev, _b in pend:
+        for r, c, host, ev, _b in pend:
             ev.synchronize()
-            a = stats.cpu().tolist()
+            a = (host if host.device.type == "cpu" else host.cpu()).tolist()
             e = EvalResult(int(a[0]), int(a[1]), a[2], a[3])
             m = {"accuracy": e.accuracy, "loss": e.ref_loss if self.cfg.compat_bad_test_loss else e.loss}
             by_round.setdefault(r, []).append((c, e.count, m))

@@ -177,7 +177,7 @@ class ServerlessRoundMixin:
         need_prev = ((self.filter is not None and not self._gossip_filter)
                      or bool(cfg.inject_byzantine) or cfg.update_clip_ratio > 0)
         self._run_deferred(block=False)  # earlier rounds' host reads whose kernels have finished
-        self._resolve_eval_local()      # last round's deferred local scores (long finished)
+        self._resolve_eval_local(block=False)   # deferred local scores that are ready
         lead_wait = self._bound_lead(r)
         self._round_now = r
         corr_wait = self._await_corrections(r)
@@ -238,6 +238,8 @@ class ServerlessRoundMixin:
             pout = self._param_out()
             info = self.gossip.end_of_round(r, W, pout,
                                             steps={c: losses[c]["batches"] for c in losses})
+        if self.eval_stream is not None:
+            self._issue_eval_local()   # the clients' local scores, behind the round-end launches
         recs += self._gossip_records(r, recs)
         verdict_rounds = []
         if self._gossip_filter:

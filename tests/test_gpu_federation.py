@@ -276,3 +276,33 @@ def test_gpu_lanes_run_has_no_unordered_stream_access(tmp_path, monkeypatch):
     D.set_runtime_for_tests(None)
     assert fed.stream_races is not None, "the checker did not run"
     assert fed.stream_races == [], "\n".join(fed.stream_races)
+
+
+def test_gpu_eval_graph_replays_match_eager(tmp_path, monkeypatch):
+    """The side stream's evaluations replayed from hipGraphs (captured on their second use)
+    return exactly the eager scores: global and deferred local accuracy / loss, every round."""
+    import json
+    from bcfl.config import FLConfig
+    from bcfl.fl import Federation
+    from bcfl.parallel import dist as D
+    outs = []
+    for graphs in ("0", "1"):
+        monkeypatch.setenv("BCFL_EVAL_GRAPHS", graphs)
+        D.set_runtime_for_tests(None)
+        out = str(tmp_path / graphs)
+        cfg = FLConfig(mode="serverless", model="bert-base-2l", dataset="imdb", num_clients=1,
+                       num_rounds=4, train_samples=64, test_samples=32, global_test_samples=64,
+                       out_dir=out, reference_prints=False, save_every=0, overlap_wgrad=False,
+                       dropout=0.1, async_gossip=True, gossip_transport="mailbox",
+                       overlap_global_eval=True, eval_local=True)
+        fed = Federation(cfg, verbose=False)
+        h = fed.run()
+        loc = [json.loads(l) for l in open(os.path.join(out, "metrics.jsonl")) if '"local_acc"' in l]
+        outs.append(([(r["global_acc"], r["global_loss"], r["distributed_acc"]) for r in h],
+                     [(x["round"], x["local_acc"], x["local_loss"]) for x in loc],
+                     len(getattr(fed, "_eval_graphs", {})), fed.flat.master.detach().cpu()))
+        D.set_runtime_for_tests(None)
+    (a_h, a_l, a_n, a_m), (b_h, b_l, b_n, b_m) = outs
+    assert a_n == 0 and b_n == 3   # global + the two local snapshot buffers
+    assert a_h == b_h and a_l == b_l
+    assert torch.equal(a_m, b_m)
