@@ -292,16 +292,24 @@ class EvalMixin:
         if not hasattr(self, "_eval_graphs"):
             self._eval_graphs, self._eval_seen = {}, set()
         key = (snap.data_ptr(), id(batches))
+        if key in self._eval_graphs and self._eval_graphs[key] is None:
+            return self.eval_trainer.evaluate_device(batches)
         ent = self._eval_graphs.get(key)
         if ent is None:
             if key not in self._eval_seen:   # first use eager: allocator and kernels warm
                 self._eval_seen.add(key)
                 return self.eval_trainer.evaluate_device(batches)
             g = torch.cuda.CUDAGraph()
-            # thread-local capture: the checkpoint writer thread may copy concurrently
-            with torch.cuda.graph(g, stream=torch.cuda.current_stream(self.device),
-                                  capture_error_mode="thread_local"):
-                out = self.eval_trainer.evaluate_device(batches)
+            try:
+                # thread-local capture: the checkpoint writer thread may copy concurrently
+                with torch.cuda.graph(g, stream=torch.cuda.current_stream(self.device),
+                                      capture_error_mode="thread_local"):
+                    out = self.eval_trainer.evaluate_device(batches)
+            except RuntimeError as e:   # a model whose forward cannot be captured stays eager
+                import warnings
+                warnings.warn(f"evaluation forward not capturable ({e}); issuing it eagerly")
+                self._eval_graphs[key] = None
+                return self.eval_trainer.evaluate_device(batches)
             ent = self._eval_graphs[key] = (g, out, batches, snap)
         ent[0].replay()
         return ent[1]

@@ -300,7 +300,8 @@ def test_gpu_eval_graph_replays_match_eager(tmp_path, monkeypatch):
         loc = [json.loads(l) for l in open(os.path.join(out, "metrics.jsonl")) if '"local_acc"' in l]
         outs.append(([(r["global_acc"], r["global_loss"], r["distributed_acc"]) for r in h],
                      [(x["round"], x["local_acc"], x["local_loss"]) for x in loc],
-                     len(getattr(fed, "_eval_graphs", {})), fed.flat.master.detach().cpu()))
+                     sum(v is not None for v in getattr(fed, "_eval_graphs", {}).values()),
+                     fed.flat.master.detach().cpu()))
         D.set_runtime_for_tests(None)
     (a_h, a_l, a_n, a_m), (b_h, b_l, b_n, b_m) = outs
     assert a_n == 0 and b_n == 3   # global + the two local snapshot buffers
