@@ -286,8 +286,10 @@ class EvalMixin:
         launches, ~2.2 ms of host issue per evaluation, which with one client per GPU the host
         spent while the training stream had nothing queued; a replay is one launch. The graph
         reads the same snapshot buffer and batches every round (both kept alive with it) and
-        runs exactly the eager kernels. ``BCFL_EVAL_GRAPHS=0`` keeps the eager issue."""
-        if os.environ.get("BCFL_EVAL_GRAPHS", "1") == "0" or not batches:
+        runs exactly the eager kernels. Opt-in (``BCFL_EVAL_GRAPHS=1``): once the round-start
+        read stopped waiting for the evaluation, replays and eager issue measured the same
+        (one-client layout, 3 interleaved reps each, ``profiles/host_issue_r6.json``)."""
+        if os.environ.get("BCFL_EVAL_GRAPHS", "0") != "1" or not batches:
             return self.eval_trainer.evaluate_device(batches)
         if not hasattr(self, "_eval_graphs"):
             self._eval_graphs, self._eval_seen = {}, set()
